@@ -1,0 +1,162 @@
+#!/usr/bin/env python
+"""Headline benchmark: Xception 299x299 serving throughput (images/s, whole node)
+and p50 batch latency on 1..8 MI355X (BASELINE.json metric/config).
+
+One process per GPU (``torch.distributed.run``), RCCL over xGMI. A timed step is
+one dynamic batch of 32 images per GPU (weak scaling, global batch 32*N):
+
+  1. ingress: rank 0 copies the uint8 batch [32N,299,299,3] host(pinned)->device;
+  2. scatter: RCCL scatter of uint8 shards (4x fewer bytes than f32)
+     straight into every rank's static engine input buffer;
+  3. forward: one hipGraph replay of the fused HIP-kernel Xception (41 launches);
+  4. gather:  RCCL gather of the fp32 logits to rank 0, D2H to host.
+
+``--ingress local`` instead has every rank H2D its own shard (host-direct mode,
+no rank-0 bottleneck). Data is synthetic (random uint8 images) and the weights are
+random-init of the exact architecture (no network for checkpoints).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+BASELINE_IMG_S = None  # the reference publishes no throughput number
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--ingress", choices=["scatter", "local"], default="scatter")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-tune", action="store_true")
+    ap.add_argument("--profile-layers", action="store_true")
+    a = ap.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from kdl.engine.xception import XceptionEngine
+    from kdl.engine.tuning import tuning_path
+    from kdl.models import xception as X
+
+    B = a.batch
+    params = X.init_params(seed=0)
+    eng = XceptionEngine(params, max_batch=B, device=dev, in_kind="u8")
+    tp = tuning_path("xception", B)
+    if tp.exists():
+        eng.load_tuning(tp)
+    elif not a.no_tune:
+        eng.autotune(B)
+    use_graph = not a.no_graph
+
+    g = torch.Generator().manual_seed(1234 + rank)
+    n_global = B * world
+    # synthetic request batch in pinned host memory (rank 0 = ingress for scatter)
+    if a.ingress == "scatter":
+        host = (torch.randint(0, 256, (n_global, 299, 299, 3), generator=g, dtype=torch.uint8).pin_memory()
+                if rank == 0 else None)
+        stage = torch.empty((n_global, 299, 299, 3), dtype=torch.uint8, device=dev) if rank == 0 else None
+    else:
+        host = torch.randint(0, 256, (B, 299, 299, 3), generator=g, dtype=torch.uint8).pin_memory()
+        stage = None
+    logits_all = torch.empty((n_global, 10), dtype=torch.float32, device=dev) if rank == 0 else None
+    out_host = torch.empty((n_global, 10), dtype=torch.float32).pin_memory() if rank == 0 else None
+    s = eng.stream
+    inp = eng.inp[:B]
+
+    def step():
+        with torch.cuda.stream(s):
+            if a.ingress == "scatter":
+                if rank == 0:
+                    stage.copy_(host, non_blocking=True)
+                if world > 1:
+                    dist.scatter(inp, list(stage.chunk(world)) if rank == 0 else None, src=0)
+                else:
+                    inp.copy_(stage)
+            else:
+                inp.copy_(host, non_blocking=True)
+            eng.launch(B, s, capture=use_graph)
+            logits = eng.logits[:B]
+            if world > 1:
+                dist.gather(logits, list(logits_all.chunk(world)) if rank == 0 else None, dst=0)
+            elif rank == 0:
+                logits_all.copy_(logits)
+            if rank == 0:
+                out_host.copy_(logits_all, non_blocking=True)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+    t0 = time.perf_counter()
+    ev[0].record(s)
+    for i in range(a.steps):
+        step()
+        ev[i + 1].record(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    lat = [ev[i].elapsed_time(ev[i + 1]) for i in range(a.steps)]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    if rank == 0:
+        ms = elapsed * 1e3 / a.steps
+        img_s = n_global * a.steps / elapsed
+        res = {
+            "metric": "images/sec (whole node) + p50 latency, Xception 299x299 at 1/2/4/8 MI355X",
+            "value": round(img_s, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "p50_latency_ms": round(statistics.median(lat), 4),
+            "p99_latency_ms": round(sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_IMG_S is None else round(img_s / BASELINE_IMG_S, 3),
+            "dtype": "bf16",
+            "data": "synthetic uint8 299x299x3 images, random-init weights",
+            "config": {"model": "Keras Xception 299x299 + clothing head (21,067,390 params)",
+                       "global_batch": n_global, "seq_len": None, "image_size": 299,
+                       "per_gpu_batch": B, "parallelism": f"dp{world}",
+                       "ingress": a.ingress, "hipgraph": use_graph},
+        }
+        print(json.dumps(res), flush=True)
+        if a.profile_layers:
+            for name, t in eng.profile(B, 10):
+                print(f"{name:28s} {t * 1e3:9.1f} us", file=sys.stderr)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,157 @@
+// pybind11 bindings of the HIP kernel library + native executor (module kdl._C).
+// Device pointers and hipStream_t travel as Python ints (torch: .data_ptr(),
+// torch.cuda.current_stream().cuda_stream); no torch headers are needed, which
+// keeps the extension a plain hipcc build (no hipify, no CUDA shims).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "kernels/launch.h"
+#include "runtime/engine.h"
+
+namespace py = pybind11;
+using namespace kdl;
+
+namespace {
+
+template <typename T>
+T* P(const py::dict& d, const char* k) {
+  if (!d.contains(k) || d[k].is_none()) return nullptr;
+  return reinterpret_cast<T*>(d[k].cast<uintptr_t>());
+}
+int I(const py::dict& d, const char* k, int def = 0) {
+  if (!d.contains(k) || d[k].is_none()) return def;
+  return d[k].cast<int>();
+}
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+ConvGemmArgs conv_args(const py::dict& d) {
+  ConvGemmArgs a{};
+  a.x = P<const uint16_t>(d, "x");
+  a.wp = P<const uint16_t>(d, "wp");
+  a.bias = P<const float>(d, "bias");
+  a.dww = P<const float>(d, "dww");
+  a.res = P<const uint16_t>(d, "res");
+  a.y = P<uint16_t>(d, "y");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W");
+  a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.M = I(d, "M");
+  a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
+  a.K = I(d, "K"); a.cin = I(d, "cin", 32); a.NF = I(d, "NF");
+  a.nstore = I(d, "nstore"); a.stride = I(d, "stride", 1);
+  a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out");
+  return a;
+}
+StemArgs stem_args(const py::dict& d) {
+  StemArgs a{};
+  a.x = P<const void>(d, "x"); a.wp = P<const uint16_t>(d, "wp");
+  a.bias = P<const float>(d, "bias"); a.y = P<uint16_t>(d, "y");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W");
+  a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.ldy = I(d, "ldy"); a.in_kind = I(d, "in_kind");
+  return a;
+}
+PoolAddArgs pool_args(const py::dict& d) {
+  PoolAddArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.res = P<const uint16_t>(d, "res"); a.y = P<uint16_t>(d, "y");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
+  a.C = I(d, "C"); a.pad_top = I(d, "pad_top"); a.pad_left = I(d, "pad_left");
+  return a;
+}
+HeadArgs head_args(const py::dict& d) {
+  HeadArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.w1t = P<const float>(d, "w1t"); a.b1 = P<const float>(d, "b1");
+  a.w2t = P<const float>(d, "w2t"); a.b2 = P<const float>(d, "b2"); a.out = P<float>(d, "out");
+  a.B = I(d, "B"); a.HW = I(d, "HW"); a.ldx = I(d, "ldx"); a.F = I(d, "F"); a.H1 = I(d, "H1");
+  a.NC = I(d, "NC");
+  return a;
+}
+ResizeArgs resize_args(const py::dict& d) {
+  ResizeArgs a{};
+  a.src = P<const uint8_t>(d, "src"); a.dst = P<uint8_t>(d, "dst");
+  a.ytab = P<const int>(d, "ytab"); a.xtab = P<const int>(d, "xtab");
+  a.SH = I(d, "SH"); a.SW = I(d, "SW"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
+  return a;
+}
+
+void chk(hipError_t e, const char* what) { check_hip(e, what); }
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "kdl MI355X (gfx950) HIP kernels and native executor";
+
+  m.def("conv_gemm", [](int mode, int cfg, py::dict d, uintptr_t s) {
+    const auto a = conv_args(d);
+    py::gil_scoped_release nogil;
+    chk(conv_gemm(mode, cfg, a, S(s)), "conv_gemm");
+  });
+  m.def("conv_gemm_config", [](int cfg) {
+    int bm = 0, bn = 0, th = 0;
+    if (conv_gemm_config(cfg, &bm, &bn, &th) != 0) throw std::out_of_range("bad conv_gemm config");
+    return py::make_tuple(bm, bn, th);
+  });
+  m.def("conv_gemm_num_configs", &conv_gemm_num_configs);
+  m.def("stem_conv", [](py::dict d, uintptr_t s) {
+    const auto a = stem_args(d);
+    py::gil_scoped_release nogil;
+    chk(stem_conv(a, S(s)), "stem_conv");
+  });
+  m.def("pool_add", [](py::dict d, uintptr_t s) {
+    const auto a = pool_args(d);
+    py::gil_scoped_release nogil;
+    chk(pool_add(a, S(s)), "pool_add");
+  });
+  m.def("head_dense", [](py::dict d, uintptr_t s) {
+    const auto a = head_args(d);
+    py::gil_scoped_release nogil;
+    chk(head_dense(a, S(s)), "head_dense");
+  });
+  m.def("resize_nearest_u8", [](py::dict d, uintptr_t s) {
+    const auto a = resize_args(d);
+    py::gil_scoped_release nogil;
+    chk(resize_nearest_u8(a, S(s)), "resize_nearest_u8");
+  });
+  m.def("u8_to_bf16_norm", [](uintptr_t x, uintptr_t y, long npix, int ldy, uintptr_t s) {
+    py::gil_scoped_release nogil;
+    chk(u8_to_bf16_norm(reinterpret_cast<const uint8_t*>(x), reinterpret_cast<uint16_t*>(y), npix, ldy, S(s)),
+        "u8_to_bf16_norm");
+  });
+
+  py::class_<Program>(m, "Program")
+      .def(py::init<>())
+      .def("add_conv_gemm", [](Program& p, const std::string& name, int mode, int cfg, py::dict d) {
+        Op op; op.kind = OP_CONV_GEMM; op.name = name; op.mode = mode; op.cfg = cfg; op.g = conv_args(d);
+        p.add(op);
+      })
+      .def("add_stem", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_STEM; op.name = name; op.st = stem_args(d); p.add(op);
+      })
+      .def("add_pool_add", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_POOL_ADD; op.name = name; op.pa = pool_args(d); p.add(op);
+      })
+      .def("add_head", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_HEAD; op.name = name; op.hd = head_args(d); p.add(op);
+      })
+      .def("add_resize", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_RESIZE; op.name = name; op.rs = resize_args(d); p.add(op);
+      })
+      .def("add_memset", [](Program& p, const std::string& name, uintptr_t ptr, size_t bytes) {
+        Op op; op.kind = OP_MEMSET; op.name = name; op.mem_ptr = reinterpret_cast<void*>(ptr);
+        op.mem_bytes = bytes; p.add(op);
+      })
+      .def("set_cfg", [](Program& p, size_t i, int cfg) { p.mutable_op(i).cfg = cfg; })
+      .def("cfg", [](const Program& p, size_t i) { return p.op(i).cfg; })
+      .def("op_names", [](const Program& p) {
+        std::vector<std::string> v;
+        for (size_t i = 0; i < p.size(); ++i) v.push_back(p.op(i).name);
+        return v;
+      })
+      .def("__len__", &Program::size)
+      .def("run", [](const Program& p, uintptr_t s) { py::gil_scoped_release nogil; p.run(S(s)); })
+      .def("capture", [](Program& p, uintptr_t s) { py::gil_scoped_release nogil; p.capture(S(s)); })
+      .def("launch", [](const Program& p, uintptr_t s) { py::gil_scoped_release nogil; p.launch(S(s)); })
+      .def("reset", &Program::reset)
+      .def_property_readonly("captured", &Program::captured)
+      .def("profile", [](const Program& p, uintptr_t s, int iters) {
+        py::gil_scoped_release nogil;
+        return p.profile(S(s), iters);
+      });
+}

@@ -1,0 +1,66 @@
+// Shared CDNA4 (gfx950) helpers for the kdl kernel library.
+//
+// Conventions used by every kernel in this directory:
+//   * activations are NHWC bf16 with the channel dimension padded to a multiple
+//     of 32 ("ldc"); padded channels always hold zeros;
+//   * MFMA is v_mfma_f32_16x16x32_bf16 (wave64, 4 fp32 accumulators per lane);
+//   * bf16 is carried as raw 16-bit patterns (uint16_t / packed in uint32_t).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kdl {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));   // one MFMA A/B fragment (8 bf16)
+typedef float f32x4 __attribute__((ext_vector_type(4)));   // one 16x16 accumulator fragment
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ float bf_lo(uint32_t d) { return __uint_as_float(d << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t d) { return __uint_as_float(d & 0xffff0000u); }
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even pack of two floats into bf16x2 (hipcc emits v_cvt_pk_bf16_f32).
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+  bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ uint16_t f2bf(float x) {
+  __bf16 b = (__bf16)x;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+// ReLU on two packed bf16 values: a negative bf16 is a negative int16 (sign bit),
+// so a signed 16-bit max against 0 is exactly ReLU (v_pk_max_i16).
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t d) {
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  s2 v = __builtin_bit_cast(s2, d);
+  s2 z = {0, 0};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, z));
+}
+
+__device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16-byte global->LDS DMA. `lds` must be wave-uniform; lane l lands at lds + 16*l.
+__device__ __forceinline__ void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void*)lds, 16, 0, 0);
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): blocks b, b+8, ... are dispatched to one XCD, so give each XCD a
+// contiguous run of logical tiles; neighbouring tiles then share an L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, local = bid >> 3;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + local;
+}
+
+}  // namespace kdl

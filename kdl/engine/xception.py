@@ -1,0 +1,311 @@
+"""MI355X executor for Keras Xception (+ clothing head).
+
+Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
+
+    stem_conv            block1_conv1 + BN + ReLU (normalisation folded, uint8 in)
+    conv_gemm MODE_CONV  block1_conv2 3x3 + BN + ReLU (implicit GEMM)
+    conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
+    conv_gemm MODE_PW    residual 1x1/2 convs + BN
+    pool_add             TF-'same' 3x3/2 max-pool + residual add
+    head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
+
+= 41 launches per forward (vs ~168 unfused TF ops), captured into
+one hipGraph per batch bucket. All buffers are allocated once for the largest
+bucket (static memory plan); smaller buckets use prefixes of the same buffers.
+The reference equivalent is TF-Serving's SavedModel session run
+(`tf-serving.dockerfile:2-5`).
+"""
+from __future__ import annotations
+
+import json
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import torch
+
+from ..models import xception as X
+from ..models.layers import tf_same_pad
+from ..ops import _lib
+from ..ops.conv import (MODE_CONV, MODE_DW, MODE_PW, ConvGemmLayer, Geometry,
+                        conv_weights_nk)
+from ..ops.pack import bn_scale_shift, pack_fragments, round_up
+
+
+@dataclass
+class Step:
+    kind: str                  # conv | stem | pool | head
+    name: str
+    layer: object = None
+    src: str = ""
+    dst: str = ""
+    res: str | None = None
+    geom: tuple = ()           # (H, W, OH, OW) per image
+    extra: dict = field(default_factory=dict)
+
+
+class XceptionEngine:
+    def __init__(self, params: dict, max_batch: int = 32, device: str | torch.device = "cuda",
+                 in_kind: str = "u8", head: X.Head = X.DEFAULT_HEAD, buckets=None,
+                 tune_file: str | Path | None = None):
+        self.device = torch.device(device)
+        self.max_batch = max_batch
+        self.in_kind = in_kind
+        self.head = head
+        self.size = X.INPUT_SIZE
+        self.buckets = sorted(set(buckets or [max_batch]))
+        assert self.buckets[-1] <= max_batch
+        self.steps: list[Step] = []
+        self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
+        self._build(params)
+        self._alloc()
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.programs: dict[int, object] = {}
+        if tune_file and Path(tune_file).exists():
+            self.load_tuning(tune_file)
+
+    # ------------------------------------------------------------------ lowering
+    def _build(self, p: dict) -> None:
+        dev = self.device
+        S = self.size
+        st = X.SPEC
+        # --- stem 1: 3x3/2 valid, 3 -> 32, folded BN (+ folded normalisation for uint8)
+        c1 = st[0].main[0]
+        s, t = bn_scale_shift(p, c1.bn)
+        w = p[f"{c1.name}/kernel"].double().reshape(27, 32).t() * s[:, None]   # [32][27], k = tap*3+c
+        if self.in_kind == "u8":
+            bias = t - w.sum(1)
+            w = w / 127.5
+        else:
+            bias = t
+        oh1 = (S - 3) // 2 + 1
+        self.stem_wp = pack_fragments(w, 2, 1).to(dev).contiguous()
+        self.stem_bias = bias.float().to(dev)
+        self.steps.append(Step("stem", c1.name, src="input", dst="stem1", geom=(S, S, oh1, oh1)))
+        self.shapes["stem1"] = (oh1, oh1, 32)
+        # --- stem 2: 3x3 valid 32 -> 64 implicit GEMM
+        c2 = st[0].main[1]
+        s, t = bn_scale_shift(p, c2.bn)
+        w = conv_weights_nk(p[f"{c2.name}/kernel"], 32) * s[:, None]
+        lay = ConvGemmLayer(c2.name, MODE_CONV, w, t, cin_pad=32, n=64, relu_out=True, device=dev)
+        h = oh1 - 2
+        self.steps.append(Step("conv", c2.name, lay, "stem1", "stem2", geom=(oh1, oh1, h, h)))
+        self.shapes["stem2"] = (h, h, 64)
+        cur, H = "stem2", h
+        for bi, blk in enumerate(st[1:], start=1):
+            if blk.kind in ("entry", "exit"):
+                rc = blk.res_conv
+                oh = (H - 1) // 2 + 1
+                rname = f"{rc.name}_out"
+                lay = self._pw(p, rc, dev)
+                self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh)))
+                self.shapes[rname] = (oh, oh, lay.ldy)
+                y = cur
+                for op in blk.main:
+                    lay = self._sep(p, op, dev)
+                    dst = f"{op.name}_out"
+                    self.steps.append(Step("conv", op.name, lay, y, dst, geom=(H, H, H, H)))
+                    self.shapes[dst] = (H, H, lay.ldy)
+                    y = dst
+                _, pt, _ = tf_same_pad(H, 3, 2)
+                out = f"block{bi + 1}_out"
+                C = self.shapes[y][2]
+                self.steps.append(Step("pool", f"block{bi + 1}_pool", src=y, dst=out, res=rname,
+                                       geom=(H, H, oh, oh), extra=dict(pad=pt, C=C)))
+                self.shapes[out] = (oh, oh, C)
+                cur, H = out, oh
+            elif blk.kind == "middle":
+                y = cur
+                for k, op in enumerate(blk.main):
+                    lay = self._sep(p, op, dev)
+                    dst = f"{op.name}_out"
+                    res = cur if k == len(blk.main) - 1 else None
+                    self.steps.append(Step("conv", op.name, lay, y, dst, res=res, geom=(H, H, H, H)))
+                    self.shapes[dst] = (H, H, lay.ldy)
+                    y = dst
+                cur = y
+            else:  # block14
+                for op in blk.main:
+                    lay = self._sep(p, op, dev)
+                    dst = f"{op.name}_out"
+                    self.steps.append(Step("conv", op.name, lay, cur, dst, geom=(H, H, H, H)))
+                    self.shapes[dst] = (H, H, lay.ldy)
+                    cur = dst
+        # --- head
+        hd = self.head
+        self.w1t = p[f"{hd.hidden}/kernel"].float().t().contiguous().to(dev)
+        self.b1 = p[f"{hd.hidden}/bias"].float().to(dev)
+        self.w2t = p[f"{hd.out}/kernel"].float().t().contiguous().to(dev)
+        self.b2 = p[f"{hd.out}/bias"].float().to(dev)
+        self.steps.append(Step("head", "head", src=cur, dst="logits", geom=(H, H, 1, 1)))
+        self.feat_buf = cur
+
+    @staticmethod
+    def _pw(p, rc, dev) -> ConvGemmLayer:
+        s, t = bn_scale_shift(p, rc.bn)
+        cin_pad = round_up(rc.cin, 32)
+        w = torch.zeros(rc.cout, cin_pad, dtype=torch.float64)
+        w[:, :rc.cin] = p[f"{rc.name}/kernel"].double()[0, 0].t() * s[:, None]
+        return ConvGemmLayer(rc.name, MODE_PW, w, t, cin_pad=cin_pad, n=rc.cout, stride=2, device=dev)
+
+    @staticmethod
+    def _sep(p, op, dev) -> ConvGemmLayer:
+        s, t = bn_scale_shift(p, op.bn)
+        cin_pad = round_up(op.cin, 32)
+        w = torch.zeros(op.cout, cin_pad, dtype=torch.float64)
+        w[:, :op.cin] = p[f"{op.name}/pointwise_kernel"].double()[0, 0].t() * s[:, None]
+        dww = torch.zeros(9, cin_pad, dtype=torch.float32)
+        dww[:, :op.cin] = p[f"{op.name}/depthwise_kernel"].float()[:, :, :, 0].reshape(9, op.cin)
+        return ConvGemmLayer(op.name, MODE_DW, w, t, cin_pad=cin_pad, n=op.cout, dww=dww,
+                             relu_in=op.relu_in, relu_out=op.relu_out, device=dev)
+
+    def _alloc(self) -> None:
+        B, S, dev = self.max_batch, self.size, self.device
+        if self.in_kind == "u8":
+            self.inp = torch.zeros((B, S, S, 3), dtype=torch.uint8, device=dev)
+        else:
+            self.inp = torch.zeros((B, S, S, 3), dtype=torch.float32, device=dev)
+        self.bufs: dict[str, torch.Tensor] = {}
+        for name, (h, w, c) in self.shapes.items():
+            self.bufs[name] = torch.zeros(B * h * w * c, dtype=torch.bfloat16, device=dev)
+        self.logits = torch.zeros((B, self.head.classes), dtype=torch.float32, device=dev)
+
+    # ------------------------------------------------------------------ programs
+    def conv_steps(self) -> list[Step]:
+        return [s for s in self.steps if s.kind == "conv"]
+
+    def _ptr(self, name: str) -> int:
+        if name == "input":
+            return _lib.ptr(self.inp)
+        if name == "logits":
+            return _lib.ptr(self.logits)
+        return _lib.ptr(self.bufs[name])
+
+    def _emit(self, prog, step: Step, b: int) -> None:
+        H, W, OH, OW = step.geom
+        if step.kind == "stem":
+            prog.add_stem(step.name, dict(x=self._ptr("input"), wp=_lib.ptr(self.stem_wp),
+                                          bias=_lib.ptr(self.stem_bias), y=self._ptr(step.dst),
+                                          B=b, H=H, W=W, OH=OH, OW=OW, ldy=32,
+                                          in_kind=0 if self.in_kind == "u8" else 1))
+        elif step.kind == "conv":
+            lay: ConvGemmLayer = step.layer
+            ldx = self.shapes[step.src][2]
+            args = lay.args(self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
+                            res=self._ptr(step.res) if step.res else None, ldx=ldx,
+                            ldr=self.shapes[step.res][2] if step.res else None)
+            prog.add_conv_gemm(step.name, lay.mode, lay.cfg, args)
+        elif step.kind == "pool":
+            prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=self._ptr(step.res),
+                                              y=self._ptr(step.dst), B=b, H=H, W=W, OH=OH, OW=OW,
+                                              C=step.extra["C"], pad_top=step.extra["pad"],
+                                              pad_left=step.extra["pad"]))
+        elif step.kind == "head":
+            hd = self.head
+            prog.add_head(step.name, dict(x=self._ptr(step.src), w1t=_lib.ptr(self.w1t),
+                                          b1=_lib.ptr(self.b1), w2t=_lib.ptr(self.w2t),
+                                          b2=_lib.ptr(self.b2), out=self._ptr("logits"),
+                                          B=b, HW=H * W, ldx=self.shapes[step.src][2],
+                                          F=hd.features, H1=hd.hidden_units, NC=hd.classes))
+
+    def program(self, b: int, capture: bool = True):
+        key = (b, capture)
+        if key in self.programs:
+            return self.programs[key]
+        assert 1 <= b <= self.max_batch
+        prog = _lib.lib().Program()
+        for step in self.steps:
+            self._emit(prog, step, b)
+        if capture:
+            with torch.cuda.device(self.device):
+                prog.capture(int(self.stream.cuda_stream))
+        self.programs[key] = prog
+        return prog
+
+    def invalidate(self) -> None:
+        self.programs.clear()
+
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        raise ValueError(f"batch {n} exceeds max bucket {self.buckets[-1]}")
+
+    # ------------------------------------------------------------------ execution
+    def launch(self, b: int, stream: torch.cuda.Stream | None = None, capture: bool = True) -> None:
+        """Run the forward for the first ``b`` images already in ``self.inp``."""
+        s = stream or self.stream
+        self.program(b, capture).launch(int(s.cuda_stream))
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, capture: bool = True) -> torch.Tensor:
+        """x: uint8 (or f32 for in_kind='f32') [n,299,299,3] on any device -> f32 logits [n,10]."""
+        n = x.shape[0]
+        assert tuple(x.shape[1:]) == (self.size, self.size, 3), x.shape
+        assert x.dtype == self.inp.dtype, (x.dtype, self.inp.dtype)
+        b = self.bucket_for(n)
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.inp[:n].copy_(x, non_blocking=True)
+            self.launch(b, self.stream, capture)
+            out = self.logits[:n].clone()
+        cur.wait_stream(self.stream)
+        return out
+
+    # ------------------------------------------------------------------ observability
+    def profile(self, b: int, iters: int = 20) -> list[tuple[str, float]]:
+        prog = self.program(b, capture=False)
+        ms = prog.profile(int(self.stream.cuda_stream), iters)
+        return list(zip(prog.op_names(), ms))
+
+    def autotune(self, b: int, iters: int = 10, verbose: bool = False) -> dict[str, int]:
+        """Pick the fastest tile config per conv layer by timing on the device."""
+        s = self.stream
+        chosen = {}
+        with torch.cuda.stream(s):
+            for step in self.conv_steps():
+                lay: ConvGemmLayer = step.layer
+                H, W, OH, OW = step.geom
+                g = Geometry(b, H, W, OH, OW)
+                x, y = self.bufs[step.src], self.bufs[step.dst]
+                res = self.bufs[step.res] if step.res else None
+                best = None
+                for cfg in lay.candidates:
+                    args = lay.args(_lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res),
+                                    ldx=self.shapes[step.src][2],
+                                    ldr=self.shapes[step.res][2] if step.res else None, cfg=cfg)
+                    C = _lib.lib()
+                    for _ in range(2):
+                        C.conv_gemm(lay.mode, cfg, args, int(s.cuda_stream))
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    for _ in range(iters):
+                        C.conv_gemm(lay.mode, cfg, args, int(s.cuda_stream))
+                    e1.record(s)
+                    e1.synchronize()
+                    t = e0.elapsed_time(e1) / iters
+                    if best is None or t < best[0]:
+                        best = (t, cfg)
+                    if verbose:
+                        print(f"  {step.name:24s} cfg {cfg}: {t * 1e3:8.1f} us", flush=True)
+                lay.cfg = best[1]
+                chosen[step.name] = best[1]
+        self.invalidate()
+        return chosen
+
+    def tuning(self) -> dict[str, int]:
+        return {s.name: s.layer.cfg for s in self.conv_steps()}
+
+    def save_tuning(self, path) -> None:
+        Path(path).write_text(json.dumps(self.tuning(), indent=1))
+
+    def load_tuning(self, path) -> None:
+        d = json.loads(Path(path).read_text())
+        for s in self.conv_steps():
+            if s.name in d and d[s.name] in s.layer.candidates:
+                s.layer.cfg = d[s.name]
+        self.invalidate()
+
+    def flops_per_image(self) -> float:
+        return 2 * 8.356e9

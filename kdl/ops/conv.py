@@ -1,0 +1,135 @@
+"""Layer objects for the fused conv-GEMM kernel family (``conv_gemm.hip``).
+
+Each ``ConvGemmLayer`` owns device-resident, BN-folded, fragment-packed weights
+and knows how to emit its launch (eagerly, for tests, or into a native
+``Program`` for hipGraph capture). The tile config is a free choice among
+``CONFIGS`` (same table as ``KDL_CONFIGS`` in the HIP source); the engine's
+autotuner picks one per layer by timing on the device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .pack import pack_fragments, pad_vec, round_up
+
+MODE_PW, MODE_CONV, MODE_DW = 0, 1, 2
+
+# (FM, FN, WGM, WGN) — keep in sync with KDL_CONFIGS in conv_gemm.hip
+CONFIGS = [(2, 2, 2, 2), (4, 2, 2, 2), (2, 4, 2, 2), (4, 4, 2, 2), (4, 6, 1, 8),
+           (2, 12, 1, 4), (4, 4, 1, 4), (2, 6, 1, 8), (8, 2, 1, 4), (4, 2, 1, 4)]
+
+
+def cfg_tile(cfg: int) -> tuple[int, int]:
+    fm, fn, wgm, wgn = CONFIGS[cfg]
+    return 16 * fm * wgm, 16 * fn * wgn
+
+
+def candidate_configs(n: int, m: int | None = None) -> list[int]:
+    """Configs whose N tile does not waste more than ~35% of the channels."""
+    out = [c for c in range(len(CONFIGS)) if round_up(n, cfg_tile(c)[1]) <= 1.35 * round_up(n, 16)]
+    if not out:  # tiny N: smallest N tile only
+        bn_min = min(cfg_tile(c)[1] for c in range(len(CONFIGS)))
+        out = [c for c in range(len(CONFIGS)) if cfg_tile(c)[1] == bn_min]
+    return out
+
+
+def default_config(mode: int, n: int, m: int) -> int:
+    cands = candidate_configs(n, m)
+    pref = [4, 6, 3, 2, 1, 0] if mode == MODE_DW else [3, 6, 1, 2, 0]
+    for c in pref:
+        if c in cands:
+            return c
+    return cands[0]
+
+
+@dataclass
+class Geometry:
+    B: int
+    H: int
+    W: int
+    OH: int
+    OW: int
+
+    @property
+    def M(self) -> int:
+        return self.B * self.OH * self.OW
+
+
+class ConvGemmLayer:
+    """A 1x1 / strided 1x1 / 3x3-valid / separable conv with fused BN(+ReLU)(+add).
+
+    ``w_nk``: folded weights [N][K] in the kernel's K order (K = padded cin for
+    pointwise, 9*padded cin for 3x3 with k = tap*cin + c). ``bias``: [N].
+    ``dww``: MODE_DW depthwise weights [9][padded cin] fp32.
+    """
+
+    def __init__(self, name: str, mode: int, w_nk: torch.Tensor, bias: torch.Tensor, *,
+                 cin_pad: int, n: int, stride: int = 1, dww: torch.Tensor | None = None,
+                 relu_in: bool = False, relu_out: bool = False, device="cuda",
+                 candidates: list[int] | None = None):
+        self.name, self.mode, self.n = name, mode, n
+        self.cin_pad, self.stride = cin_pad, stride
+        self.relu_in, self.relu_out = relu_in, relu_out
+        self.K = w_nk.shape[1]
+        assert self.K % 32 == 0, (name, self.K)
+        self.ldy = round_up(n, 32)
+        self.candidates = candidates if candidates is not None else candidate_configs(n)
+        self.nf_max = max(round_up(n, cfg_tile(c)[1]) // 16 for c in self.candidates)
+        self.cfg = default_config(mode, n, 0) if candidates is None else self.candidates[0]
+        if self.cfg not in self.candidates:
+            self.cfg = self.candidates[0]
+        self.wp = pack_fragments(w_nk, self.nf_max, self.K // 32).to(device).contiguous()
+        self.bias = pad_vec(bias, self.nf_max * 16).to(device)
+        self.dww = None
+        if mode == MODE_DW:
+            assert dww is not None and dww.shape == (9, cin_pad)
+            self.dww = dww.float().contiguous().to(device)
+        # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
+        self.w_ref = w_nk.to(torch.bfloat16).float()
+
+    def nf(self, cfg: int | None = None) -> int:
+        cfg = self.cfg if cfg is None else cfg
+        return round_up(self.n, cfg_tile(cfg)[1]) // 16
+
+    def args(self, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
+             ldr: int | None = None, cfg: int | None = None) -> dict:
+        return dict(x=x, wp=_lib.ptr(self.wp), bias=_lib.ptr(self.bias),
+                    dww=_lib.ptr(self.dww), res=res, y=y,
+                    B=g.B, H=g.H, W=g.W, OH=g.OH, OW=g.OW, M=g.M,
+                    ldx=ldx if ldx is not None else self.cin_pad, ldy=self.ldy,
+                    ldr=ldr if ldr is not None else self.ldy,
+                    K=self.K, cin=self.cin_pad, NF=self.nf(cfg), nstore=self.ldy,
+                    stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out))
+
+    def launch(self, x: torch.Tensor, y: torch.Tensor, g: Geometry, res: torch.Tensor | None = None,
+               cfg: int | None = None, stream=None) -> None:
+        """Eager launch on torch tensors (shape-checked on the host first)."""
+        self.check(x, y, g, res)
+        cfg = self.cfg if cfg is None else cfg
+        _lib.lib().conv_gemm(self.mode, cfg, self.args(_lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res), cfg=cfg),
+                             _lib.stream_ptr(stream))
+
+    def check(self, x, y, g: Geometry, res=None) -> None:
+        assert x.dtype == torch.bfloat16 and y.dtype == torch.bfloat16
+        assert x.is_contiguous() and y.is_contiguous()
+        assert x.numel() >= g.B * g.H * g.W * self.cin_pad, (self.name, x.shape)
+        assert y.numel() >= g.M * self.ldy, (self.name, y.shape)
+        if self.mode == MODE_DW:
+            assert g.OH == g.H and g.OW == g.W
+        elif self.mode == MODE_CONV:
+            assert g.OH == g.H - 2 and g.OW == g.W - 2
+        else:
+            assert g.OH == (g.H - 1) // self.stride + 1 and g.OW == (g.W - 1) // self.stride + 1
+        if res is not None:
+            assert res.dtype == torch.bfloat16 and res.numel() >= g.M * self.ldy
+
+
+def conv_weights_nk(kernel_hwio: torch.Tensor, cin_pad: int) -> torch.Tensor:
+    """Keras HWIO kernel -> [N][K] with k = (dy*kw+dx)*cin_pad + c."""
+    kh, kw, cin, cout = kernel_hwio.shape
+    w = torch.zeros(kh * kw, cin_pad, cout, dtype=torch.float64)
+    w[:, :cin, :] = kernel_hwio.double().reshape(kh * kw, cin, cout)
+    return w.reshape(kh * kw * cin_pad, cout).t().contiguous()

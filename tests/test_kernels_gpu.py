@@ -1,0 +1,182 @@
+"""Numerics of every HIP kernel against fp32 torch references (run on MI355X).
+
+Shapes cover the awkward cases from SURVEY.md §2.5: ragged M (19x19xB), the
+N=K=728 tails (padded to 736), stride-2 residual convs, the asymmetric TF pool
+pad at 74->37, and every autotuner tile config.
+"""
+import pytest
+import torch
+
+from kdl.ops import _lib
+from kdl.ops.conv import MODE_CONV, MODE_DW, MODE_PW, ConvGemmLayer, Geometry, cfg_tile
+from kdl.ops.pack import round_up
+from kdl.ops.reference import conv_gemm_ref, head_ref, pool_add_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rand_act(shape, ldc, c, gen):
+    x = torch.zeros(*shape, ldc)
+    x[..., :c] = torch.randn(*shape, c, generator=gen)
+    return x.to(torch.bfloat16).to(DEV).contiguous()
+
+
+def _layer(mode, cin, n, gen, stride=1, relu_in=False, relu_out=False):
+    cin_pad = round_up(cin, 32)
+    k = 9 * cin_pad if mode == MODE_CONV else cin_pad
+    w = torch.zeros(n, k, dtype=torch.float64)
+    if mode == MODE_CONV:
+        w3 = torch.randn(n, 9, cin, generator=gen, dtype=torch.float64) / (9 * cin) ** 0.5
+        w.view(n, 9, cin_pad)[:, :, :cin] = w3
+    else:
+        w[:, :cin] = torch.randn(n, cin, generator=gen, dtype=torch.float64) / cin ** 0.5
+    bias = torch.randn(n, generator=gen) * 0.1
+    dww = None
+    if mode == MODE_DW:
+        dww = torch.zeros(9, cin_pad)
+        dww[:, :cin] = torch.randn(9, cin, generator=gen) / 3
+    return ConvGemmLayer("t", mode, w, bias, cin_pad=cin_pad, n=n, stride=stride, dww=dww,
+                         relu_in=relu_in, relu_out=relu_out, device=DEV)
+
+
+def _check(y, ref, n, tol=2e-2):
+    yf = y.float().view(ref.shape)
+    err = (yf - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+    # padded output channels must stay exactly zero
+    if yf.shape[1] > n:
+        assert yf[:, n:].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("cin,n,H,stride", [(64, 128, 37, 2), (728, 1024, 19, 2), (256, 728, 37, 2),
+                                            (128, 256, 10, 1)])
+def test_conv_gemm_pointwise(cin, n, H, stride):
+    gen = torch.Generator().manual_seed(1)
+    lay = _layer(MODE_PW, cin, n, gen, stride=stride)
+    B = 3
+    OH = (H - 1) // stride + 1
+    g = Geometry(B, H, H, OH, OH)
+    x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
+    ref = conv_gemm_ref(lay, x, g)
+    for cfg in lay.candidates:
+        y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lay.launch(x, y, g, cfg=cfg)
+        torch.cuda.synchronize()
+        _check(y, ref, n)
+
+
+def test_conv_gemm_conv3x3():
+    gen = torch.Generator().manual_seed(2)
+    lay = _layer(MODE_CONV, 32, 64, gen, relu_out=True)
+    B, H = 2, 23
+    g = Geometry(B, H, H, H - 2, H - 2)
+    x = _rand_act((B, H, H), 32, 32, gen)
+    ref = conv_gemm_ref(lay, x, g)
+    for cfg in lay.candidates:
+        y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+        lay.launch(x, y, g, cfg=cfg)
+        torch.cuda.synchronize()
+        _check(y, ref, 64)
+
+
+@pytest.mark.parametrize("cin,n,H,relu_in,relu_out,with_res", [
+    (728, 728, 19, True, True, False),
+    (728, 728, 19, False, False, True),
+    (64, 128, 29, False, True, False),
+    (256, 728, 37, True, True, False),
+    (1024, 1536, 10, False, True, False),
+])
+def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
+    gen = torch.Generator().manual_seed(3)
+    lay = _layer(MODE_DW, cin, n, gen, relu_in=relu_in, relu_out=relu_out)
+    B = 2
+    g = Geometry(B, H, H, H, H)
+    x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
+    res = _rand_act((B, H, H), lay.ldy, n, gen) if with_res else None
+    ref = conv_gemm_ref(lay, x, g, res=res)
+    for cfg in lay.candidates:
+        y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+        lay.launch(x, y, g, res=res, cfg=cfg)
+        torch.cuda.synchronize()
+        _check(y, ref, n)
+
+
+def test_conv_gemm_repeat_race_screen():
+    """Same launch many times: LDS/DMA ordering bugs show up as run-to-run diffs."""
+    gen = torch.Generator().manual_seed(4)
+    lay = _layer(MODE_DW, 728, 728, gen, relu_in=True, relu_out=True)
+    B, H = 8, 19
+    g = Geometry(B, H, H, H, H)
+    x = _rand_act((B, H, H), lay.cin_pad, 728, gen)
+    for cfg in lay.candidates:
+        y0 = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+        lay.launch(x, y0, g, cfg=cfg)
+        for _ in range(10):
+            y = torch.zeros_like(y0)
+            lay.launch(x, y, g, cfg=cfg)
+            torch.cuda.synchronize()
+            assert torch.equal(y, y0), f"cfg {cfg} nondeterministic"
+
+
+@pytest.mark.parametrize("in_kind", ["u8", "f32"])
+def test_stem(in_kind):
+    gen = torch.Generator().manual_seed(5)
+    B, H = 2, 299
+    OH = (H - 3) // 2 + 1
+    w = torch.randn(3, 3, 3, 32, generator=gen, dtype=torch.float64) * 0.2
+    bias = torch.randn(32, generator=gen, dtype=torch.float64) * 0.1
+    img = torch.randint(0, 256, (B, H, H, 3), generator=gen, dtype=torch.uint8)
+    xn = img.double() / 127.5 - 1.0
+    ref = torch.relu(torch.nn.functional.conv2d(xn.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), stride=2)
+                     + bias[None, :, None, None]).permute(0, 2, 3, 1).reshape(-1, 32).float()
+    wk = w.reshape(27, 32).t()
+    if in_kind == "u8":
+        b2, wk, x = bias - wk.sum(1), wk / 127.5, img.to(DEV)
+    else:
+        b2, x = bias, xn.float().to(DEV)
+    from kdl.ops.pack import pack_fragments
+    wp = pack_fragments(wk, 2, 1).to(DEV)
+    bb = b2.float().to(DEV)
+    y = torch.zeros(B * OH * OH * 32, dtype=torch.bfloat16, device=DEV)
+    _lib.lib().stem_conv(dict(x=_lib.ptr(x), wp=_lib.ptr(wp), bias=_lib.ptr(bb), y=_lib.ptr(y), B=B, H=H, W=H,
+                              OH=OH, OW=OH, ldy=32, in_kind=0 if in_kind == "u8" else 1),
+                         _lib.stream_ptr())
+    torch.cuda.synchronize()
+    err = (y.float().cpu().view(-1, 32) - ref).abs().max().item()
+    assert err < 0.03 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("H,C,with_res", [(147, 128, True), (74, 256, True), (37, 736, False), (19, 1024, True)])
+def test_pool_add(H, C, with_res):
+    from kdl.models.layers import tf_same_pad
+    gen = torch.Generator().manual_seed(6)
+    B = 2
+    OH, pt, _ = tf_same_pad(H, 3, 2)
+    x = torch.randn(B * H * H * C, generator=gen).to(torch.bfloat16).to(DEV)
+    res = torch.randn(B * OH * OH * C, generator=gen).to(torch.bfloat16).to(DEV) if with_res else None
+    y = torch.zeros(B * OH * OH * C, dtype=torch.bfloat16, device=DEV)
+    _lib.lib().pool_add(dict(x=_lib.ptr(x), res=_lib.ptr(res), y=_lib.ptr(y), B=B, H=H, W=H, OH=OH, OW=OH,
+                             C=C, pad_top=pt, pad_left=pt), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    ref = pool_add_ref(x, res, B, H, H, OH, OH, C, pt)
+    err = (y.float().view(-1, C) - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item(), err
+
+
+def test_head():
+    gen = torch.Generator().manual_seed(7)
+    B, HW, F_, H1, NC = 5, 100, 2048, 100, 10
+    x = torch.randn(B * HW * F_, generator=gen).to(torch.bfloat16).to(DEV)
+    w1t = (torch.randn(H1, F_, generator=gen) / 45).to(DEV)
+    b1 = (torch.randn(H1, generator=gen) * 0.1).to(DEV)
+    w2t = (torch.randn(NC, H1, generator=gen) / 10).to(DEV)
+    b2 = (torch.randn(NC, generator=gen) * 0.1).to(DEV)
+    out = torch.zeros(B, NC, device=DEV)
+    _lib.lib().head_dense(dict(x=_lib.ptr(x), w1t=_lib.ptr(w1t), b1=_lib.ptr(b1), w2t=_lib.ptr(w2t),
+                               b2=_lib.ptr(b2), out=_lib.ptr(out), B=B, HW=HW, ldx=F_, F=F_, H1=H1, NC=NC),
+                          _lib.stream_ptr())
+    torch.cuda.synchronize()
+    ref = head_ref(x, B, HW, F_, F_, w1t, b1, w2t, b2)
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-3), (out - ref).abs().max()
