@@ -57,8 +57,8 @@ PoolAddArgs pool_args(const py::dict& d) {
 }
 HeadArgs head_args(const py::dict& d) {
   HeadArgs a{};
-  a.x = P<const uint16_t>(d, "x"); a.w1t = P<const float>(d, "w1t"); a.b1 = P<const float>(d, "b1");
-  a.w2t = P<const float>(d, "w2t"); a.b2 = P<const float>(d, "b2"); a.out = P<float>(d, "out");
+  a.x = P<const uint16_t>(d, "x"); a.w1 = P<const float>(d, "w1"); a.b1 = P<const float>(d, "b1");
+  a.w2 = P<const float>(d, "w2"); a.b2 = P<const float>(d, "b2"); a.out = P<float>(d, "out");
   a.B = I(d, "B"); a.HW = I(d, "HW"); a.ldx = I(d, "ldx"); a.F = I(d, "F"); a.H1 = I(d, "H1");
   a.NC = I(d, "NC");
   return a;
@@ -68,6 +68,13 @@ ResizeArgs resize_args(const py::dict& d) {
   a.src = P<const uint8_t>(d, "src"); a.dst = P<uint8_t>(d, "dst");
   a.ytab = P<const int>(d, "ytab"); a.xtab = P<const int>(d, "xtab");
   a.SH = I(d, "SH"); a.SW = I(d, "SW"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
+  return a;
+}
+
+DwArgs dw_args(const py::dict& d) {
+  DwArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.w = P<const float>(d, "w"); a.y = P<uint16_t>(d, "y");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.C = I(d, "C"); a.relu_in = I(d, "relu_in");
   return a;
 }
 
@@ -89,6 +96,11 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(bm, bn, th);
   });
   m.def("conv_gemm_num_configs", &conv_gemm_num_configs);
+  m.def("dw3x3", [](py::dict d, uintptr_t s) {
+    const auto a = dw_args(d);
+    py::gil_scoped_release nogil;
+    chk(dw3x3(a, S(s)), "dw3x3");
+  });
   m.def("stem_conv", [](py::dict d, uintptr_t s) {
     const auto a = stem_args(d);
     py::gil_scoped_release nogil;
@@ -132,6 +144,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_resize", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_RESIZE; op.name = name; op.rs = resize_args(d); p.add(op);
+      })
+      .def("add_dw", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_DW; op.name = name; op.dw = dw_args(d); p.add(op);
       })
       .def("add_memset", [](Program& p, const std::string& name, uintptr_t ptr, size_t bytes) {
         Op op; op.kind = OP_MEMSET; op.name = name; op.mem_ptr = reinterpret_cast<void*>(ptr);

@@ -30,6 +30,16 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 int conv_gemm_config(int cfg, int* bm, int* bn, int* threads);
 int conv_gemm_num_configs();
 
+// Depthwise 3x3 'same' (+ReLU on load): NHWC bf16 [B][H][W][C] -> same layout.
+struct DwArgs {
+  const uint16_t* x;
+  const float* w;         // [9][C] fp32
+  uint16_t* y;
+  int B, H, W, C;         // C = padded channel stride (multiple of 8)
+  int relu_in;
+};
+hipError_t dw3x3(const DwArgs& a, hipStream_t s);
+
 // Stem: 3x3 stride-2 'valid' conv, 3 input channels -> 32, + bias + ReLU.
 // in_kind: 0 = uint8 HWC pixels (Xception normalisation folded into weights),
 //          1 = fp32 HWC already preprocessed (TF-Serving compat input).
@@ -56,9 +66,9 @@ hipError_t pool_add(const PoolAddArgs& a, hipStream_t s);
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {
   const uint16_t* x;      // [B][HW][ldx] bf16
-  const float* w1t;       // [H1][F] fp32 (transposed Keras kernel)
+  const float* w1;        // [F][H1] fp32 (Keras Dense kernel layout)
   const float* b1;        // [H1]
-  const float* w2t;       // [NC][H1]
+  const float* w2;        // [H1][NC]
   const float* b2;        // [NC]
   float* out;             // [B][NC]
   int B, HW, ldx, F, H1, NC;

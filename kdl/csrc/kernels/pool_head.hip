@@ -60,18 +60,23 @@ hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// One 256-thread block per image. GAP accumulates in fp32; the two dense layers
-// are wave-parallel dot products with 64-lane shuffle reductions.
-__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+// One 1024-thread block per image (the head is latency-bound: parallelise every
+// reduction). GAP: 4 pixel groups x 256 channel-chunks, partial sums through LDS.
+// Dense1 (Keras [F][H1] layout, coalesced across outputs): 8 k-slices x 128
+// outputs, reduced through LDS. Dense2 is tiny.
+__global__ __launch_bounds__(1024) void head_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
-  float* feat = hsm;           // [F]
-  float* hid = hsm + a.F;      // [H1]
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* part = hsm;                 // [4][F] GAP partials, later [8][128] dense partials
+  float* feat = hsm + 4 * a.F;       // [F]
+  float* hid = feat + a.F;           // [H1]
+  const int b = blockIdx.x, tid = threadIdx.x;
   const uint16_t* xb = a.x + (long)b * a.HW * a.ldx;
-  const float inv = 1.0f / (float)a.HW;
-  for (int c8 = tid; c8 < a.F / 8; c8 += 256) {
+  const int nchunk = a.F / 8;
+  for (int i = tid; i < 4 * nchunk; i += 1024) {
+    const int c8 = i % nchunk, pg = i / nchunk;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int p = 0; p < a.HW; ++p) {
+#pragma unroll 5
+    for (int p = pg; p < a.HW; p += 4) {
       const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx + c8 * 8);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
@@ -80,35 +85,44 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
       }
     }
 #pragma unroll
-    for (int d = 0; d < 8; ++d) feat[c8 * 8 + d] = s[d] * inv;
+    for (int d = 0; d < 8; ++d) part[pg * a.F + c8 * 8 + d] = s[d];
   }
   __syncthreads();
-  for (int o = wave; o < a.H1; o += 4) {
-    const float* w = a.w1t + (long)o * a.F;
+  const float inv = 1.0f / (float)a.HW;
+  for (int k = tid; k < a.F; k += 1024)
+    feat[k] = (part[k] + part[a.F + k] + part[2 * a.F + k] + part[3 * a.F + k]) * inv;
+  __syncthreads();
+  {
+    const int o = tid & 127, sl = tid >> 7;   // 8 slices
+    const int klen = a.F / 8;
     float s = 0.f;
-    for (int k = lane * 4; k < a.F; k += 256) {
-      const float4 wv = *(const float4*)(w + k);
-      s += wv.x * feat[k] + wv.y * feat[k + 1] + wv.z * feat[k + 2] + wv.w * feat[k + 3];
+    if (o < a.H1) {
+      const float* w = a.w1 + (long)(sl * klen) * a.H1 + o;
+      const float* f = feat + sl * klen;
+#pragma unroll 8
+      for (int k = 0; k < klen; ++k) s += f[k] * w[(long)k * a.H1];
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) hid[o] = fmaxf(s + a.b1[o], 0.f);
+    part[sl * 128 + o] = s;
   }
   __syncthreads();
-  for (int o = wave; o < a.NC; o += 4) {
-    const float* w = a.w2t + (long)o * a.H1;
-    float s = 0.f;
-    for (int k = lane; k < a.H1; k += 64) s += w[k] * hid[k];
+  if (tid < a.H1) {
+    float s = a.b1[tid];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) a.out[(long)b * a.NC + o] = s + a.b2[o];
+    for (int sl = 0; sl < 8; ++sl) s += part[sl * 128 + tid];
+    hid[tid] = fmaxf(s, 0.f);
+  }
+  __syncthreads();
+  if (tid < a.NC) {
+    float s = a.b2[tid];
+    for (int k = 0; k < a.H1; ++k) s += hid[k] * a.w2[(long)k * a.NC + tid];
+    a.out[(long)b * a.NC + tid] = s;
   }
 }
 
 hipError_t head_dense(const HeadArgs& a, hipStream_t s) {
-  if (a.F % 256 != 0 || a.ldx % 8 != 0) return hipErrorInvalidValue;
-  const size_t smem = (size_t)(a.F + a.H1) * sizeof(float);
-  hipLaunchKernelGGL(head_kernel, dim3(a.B), dim3(256), smem, s, a);
+  if (a.F % 64 != 0 || a.ldx % 8 != 0 || a.H1 > 128 || a.NC > 1024) return hipErrorInvalidValue;
+  const size_t smem = (size_t)(4 * a.F + a.F + a.H1) * sizeof(float);
+  hipLaunchKernelGGL(head_kernel, dim3(a.B), dim3(1024), smem, s, a);
   return hipGetLastError();
 }
 

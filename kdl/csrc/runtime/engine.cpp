@@ -16,6 +16,7 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_HEAD: return head_dense(op.hd, s);
     case OP_RESIZE: return resize_nearest_u8(op.rs, s);
     case OP_MEMSET: return hipMemsetAsync(op.mem_ptr, 0, op.mem_bytes, s);
+    case OP_DW: return dw3x3(op.dw, s);
   }
   return hipErrorInvalidValue;
 }

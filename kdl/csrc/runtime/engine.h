@@ -15,7 +15,7 @@
 
 namespace kdl {
 
-enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5 };
+enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6 };
 
 struct Op {
   OpKind kind;
@@ -26,6 +26,7 @@ struct Op {
   PoolAddArgs pa{};
   HeadArgs hd{};
   ResizeArgs rs{};
+  DwArgs dw{};
   void* mem_ptr = nullptr;
   size_t mem_bytes = 0;
 };

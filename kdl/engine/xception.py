@@ -133,9 +133,9 @@ class XceptionEngine:
                     cur = dst
         # --- head
         hd = self.head
-        self.w1t = p[f"{hd.hidden}/kernel"].float().t().contiguous().to(dev)
+        self.w1 = p[f"{hd.hidden}/kernel"].float().contiguous().to(dev)   # Keras [F][H1]
         self.b1 = p[f"{hd.hidden}/bias"].float().to(dev)
-        self.w2t = p[f"{hd.out}/kernel"].float().t().contiguous().to(dev)
+        self.w2 = p[f"{hd.out}/kernel"].float().contiguous().to(dev)      # Keras [H1][NC]
         self.b2 = p[f"{hd.out}/bias"].float().to(dev)
         self.steps.append(Step("head", "head", src=cur, dst="logits", geom=(H, H, 1, 1)))
         self.feat_buf = cur
@@ -169,6 +169,13 @@ class XceptionEngine:
         for name, (h, w, c) in self.shapes.items():
             self.bufs[name] = torch.zeros(B * h * w * c, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros((B, self.head.classes), dtype=torch.float32, device=dev)
+        # scratch for split separable convs (depthwise output), sized for the largest layer
+        n = 1
+        for st in self.conv_steps():
+            if st.layer.mode == MODE_DW:
+                H, W, _, _ = st.geom
+                n = max(n, B * H * W * st.layer.cin_pad)
+        self.dwtmp = torch.zeros(n, dtype=torch.bfloat16, device=dev)
 
     # ------------------------------------------------------------------ programs
     def conv_steps(self) -> list[Step]:
@@ -190,11 +197,9 @@ class XceptionEngine:
                                           in_kind=0 if self.in_kind == "u8" else 1))
         elif step.kind == "conv":
             lay: ConvGemmLayer = step.layer
-            ldx = self.shapes[step.src][2]
-            args = lay.args(self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
-                            res=self._ptr(step.res) if step.res else None, ldx=ldx,
-                            ldr=self.shapes[step.res][2] if step.res else None)
-            prog.add_conv_gemm(step.name, lay.mode, lay.cfg, args)
+            lay.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
+                     res=self._ptr(step.res) if step.res else None, ldx=self.shapes[step.src][2],
+                     ldr=self.shapes[step.res][2] if step.res else None, tmp=_lib.ptr(self.dwtmp))
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=self._ptr(step.res),
                                               y=self._ptr(step.dst), B=b, H=H, W=W, OH=OH, OW=OW,
@@ -202,8 +207,8 @@ class XceptionEngine:
                                               pad_left=step.extra["pad"]))
         elif step.kind == "head":
             hd = self.head
-            prog.add_head(step.name, dict(x=self._ptr(step.src), w1t=_lib.ptr(self.w1t),
-                                          b1=_lib.ptr(self.b1), w2t=_lib.ptr(self.w2t),
+            prog.add_head(step.name, dict(x=self._ptr(step.src), w1=_lib.ptr(self.w1),
+                                          b1=_lib.ptr(self.b1), w2=_lib.ptr(self.w2),
                                           b2=_lib.ptr(self.b2), out=self._ptr("logits"),
                                           B=b, HW=H * W, ldx=self.shapes[step.src][2],
                                           F=hd.features, H1=hd.hidden_units, NC=hd.classes))
@@ -271,31 +276,32 @@ class XceptionEngine:
                 x, y = self.bufs[step.src], self.bufs[step.dst]
                 res = self.bufs[step.res] if step.res else None
                 best = None
-                for cfg in lay.candidates:
-                    args = lay.args(_lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res),
-                                    ldx=self.shapes[step.src][2],
-                                    ldr=self.shapes[step.res][2] if step.res else None, cfg=cfg)
-                    C = _lib.lib()
+                for split, cfg in lay.variants():
+                    def run():
+                        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res),
+                                 ldx=self.shapes[step.src][2],
+                                 ldr=self.shapes[step.res][2] if step.res else None,
+                                 tmp=_lib.ptr(self.dwtmp), split=split, cfg=cfg)
                     for _ in range(2):
-                        C.conv_gemm(lay.mode, cfg, args, int(s.cuda_stream))
+                        run()
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(s)
                     for _ in range(iters):
-                        C.conv_gemm(lay.mode, cfg, args, int(s.cuda_stream))
+                        run()
                     e1.record(s)
                     e1.synchronize()
                     t = e0.elapsed_time(e1) / iters
                     if best is None or t < best[0]:
-                        best = (t, cfg)
+                        best = (t, split, cfg)
                     if verbose:
-                        print(f"  {step.name:24s} cfg {cfg}: {t * 1e3:8.1f} us", flush=True)
-                lay.cfg = best[1]
-                chosen[step.name] = best[1]
+                        print(f"  {step.name:24s} split={int(split)} cfg {cfg}: {t * 1e3:8.1f} us", flush=True)
+                lay.split, lay.cfg = best[1], best[2]
+                chosen[step.name] = [int(best[1]), best[2]]
         self.invalidate()
         return chosen
 
-    def tuning(self) -> dict[str, int]:
-        return {s.name: s.layer.cfg for s in self.conv_steps()}
+    def tuning(self) -> dict[str, list[int]]:
+        return {s.name: [int(s.layer.split), s.layer.cfg] for s in self.conv_steps()}
 
     def save_tuning(self, path) -> None:
         Path(path).write_text(json.dumps(self.tuning(), indent=1))
@@ -303,8 +309,12 @@ class XceptionEngine:
     def load_tuning(self, path) -> None:
         d = json.loads(Path(path).read_text())
         for s in self.conv_steps():
-            if s.name in d and d[s.name] in s.layer.candidates:
-                s.layer.cfg = d[s.name]
+            v = d.get(s.name)
+            if v is None:
+                continue
+            split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
+            if cfg in s.layer.candidates and (not split or s.layer.mode == MODE_DW):
+                s.layer.split, s.layer.cfg = split, cfg
         self.invalidate()
 
     def flops_per_image(self) -> float:

@@ -89,6 +89,45 @@ class ConvGemmLayer:
             self.dww = dww.float().contiguous().to(device)
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
         self.w_ref = w_nk.to(torch.bfloat16).float()
+        # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
+        # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
+        self.split = False
+
+    def variants(self) -> list[tuple[bool, int]]:
+        v = [(False, c) for c in self.candidates]
+        if self.mode == MODE_DW:
+            v += [(True, c) for c in self.candidates]
+        return v
+
+    def dw_args(self, x: int, tmp: int, g: Geometry, ldx: int | None = None) -> dict:
+        assert (ldx or self.cin_pad) == self.cin_pad
+        return dict(x=x, w=_lib.ptr(self.dww), y=tmp, B=g.B, H=g.H, W=g.W, C=self.cin_pad,
+                    relu_in=int(self.relu_in))
+
+    def emit(self, prog, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
+             ldr: int | None = None, tmp: int | None = None, split: bool | None = None,
+             cfg: int | None = None) -> None:
+        """Append this layer's launches to a native Program (or launch now if prog is None)."""
+        split = self.split if split is None else split
+        cfg = self.cfg if cfg is None else cfg
+        C = _lib.lib()
+        if self.mode == MODE_DW and split:
+            assert tmp is not None, "split separable conv needs a scratch buffer"
+            da = self.dw_args(x, tmp, g, ldx)
+            ga = self.args(tmp, y, g, res, ldx=self.cin_pad, ldr=ldr, cfg=cfg)
+            if prog is None:
+                s = _lib.stream_ptr()
+                C.dw3x3(da, s)
+                C.conv_gemm(MODE_PW, cfg, ga, s)
+            else:
+                prog.add_dw(self.name + "/dw", da)
+                prog.add_conv_gemm(self.name, MODE_PW, cfg, ga)
+            return
+        ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg)
+        if prog is None:
+            C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
+        else:
+            prog.add_conv_gemm(self.name, self.mode, cfg, ga)
 
     def nf(self, cfg: int | None = None) -> int:
         cfg = self.cfg if cfg is None else cfg
@@ -105,12 +144,14 @@ class ConvGemmLayer:
                     stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out))
 
     def launch(self, x: torch.Tensor, y: torch.Tensor, g: Geometry, res: torch.Tensor | None = None,
-               cfg: int | None = None, stream=None) -> None:
+               cfg: int | None = None, split: bool = False, tmp: torch.Tensor | None = None) -> None:
         """Eager launch on torch tensors (shape-checked on the host first)."""
         self.check(x, y, g, res)
-        cfg = self.cfg if cfg is None else cfg
-        _lib.lib().conv_gemm(self.mode, cfg, self.args(_lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res), cfg=cfg),
-                             _lib.stream_ptr(stream))
+        if split:
+            if tmp is None:
+                tmp = torch.empty(g.M * self.cin_pad, dtype=torch.bfloat16, device=x.device)
+            assert tmp.numel() >= g.M * self.cin_pad
+        self.emit(None, _lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res), tmp=_lib.ptr(tmp), split=split, cfg=cfg)
 
     def check(self, x, y, g: Geometry, res=None) -> None:
         assert x.dtype == torch.bfloat16 and y.dtype == torch.bfloat16

@@ -58,7 +58,8 @@ def pool_add_ref(x: torch.Tensor, res: torch.Tensor | None, B, H, W, OH, OW, C, 
     return y.reshape(B * OH * OW, C)
 
 
-def head_ref(x: torch.Tensor, B, HW, ldx, F_, w1t, b1, w2t, b2) -> torch.Tensor:
+def head_ref(x: torch.Tensor, B, HW, ldx, F_, w1, b1, w2, b2) -> torch.Tensor:
+    """w1: Keras [F][H1], w2: [H1][NC]."""
     g = x.float().view(B, HW, ldx)[..., :F_].mean(1)
-    h = torch.relu(g @ w1t.t() + b1)
-    return h @ w2t.t() + b2
+    h = torch.relu(g @ w1 + b1)
+    return h @ w2 + b2

@@ -96,9 +96,9 @@ def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
     x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
     res = _rand_act((B, H, H), lay.ldy, n, gen) if with_res else None
     ref = conv_gemm_ref(lay, x, g, res=res)
-    for cfg in lay.candidates:
+    for split, cfg in lay.variants():
         y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
-        lay.launch(x, y, g, res=res, cfg=cfg)
+        lay.launch(x, y, g, res=res, cfg=cfg, split=split)
         torch.cuda.synchronize()
         _check(y, ref, n)
 
@@ -110,12 +110,12 @@ def test_conv_gemm_repeat_race_screen():
     B, H = 8, 19
     g = Geometry(B, H, H, H, H)
     x = _rand_act((B, H, H), lay.cin_pad, 728, gen)
-    for cfg in lay.candidates:
+    for split, cfg in lay.variants():
         y0 = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
-        lay.launch(x, y0, g, cfg=cfg)
+        lay.launch(x, y0, g, cfg=cfg, split=split)
         for _ in range(10):
             y = torch.zeros_like(y0)
-            lay.launch(x, y, g, cfg=cfg)
+            lay.launch(x, y, g, cfg=cfg, split=split)
             torch.cuda.synchronize()
             assert torch.equal(y, y0), f"cfg {cfg} nondeterministic"
 
@@ -169,14 +169,14 @@ def test_head():
     gen = torch.Generator().manual_seed(7)
     B, HW, F_, H1, NC = 5, 100, 2048, 100, 10
     x = torch.randn(B * HW * F_, generator=gen).to(torch.bfloat16).to(DEV)
-    w1t = (torch.randn(H1, F_, generator=gen) / 45).to(DEV)
+    w1 = (torch.randn(F_, H1, generator=gen) / 45).to(DEV)
     b1 = (torch.randn(H1, generator=gen) * 0.1).to(DEV)
-    w2t = (torch.randn(NC, H1, generator=gen) / 10).to(DEV)
+    w2 = (torch.randn(H1, NC, generator=gen) / 10).to(DEV)
     b2 = (torch.randn(NC, generator=gen) * 0.1).to(DEV)
     out = torch.zeros(B, NC, device=DEV)
-    _lib.lib().head_dense(dict(x=_lib.ptr(x), w1t=_lib.ptr(w1t), b1=_lib.ptr(b1), w2t=_lib.ptr(w2t),
+    _lib.lib().head_dense(dict(x=_lib.ptr(x), w1=_lib.ptr(w1), b1=_lib.ptr(b1), w2=_lib.ptr(w2),
                                b2=_lib.ptr(b2), out=_lib.ptr(out), B=B, HW=HW, ldx=F_, F=F_, H1=H1, NC=NC),
                           _lib.stream_ptr())
     torch.cuda.synchronize()
-    ref = head_ref(x, B, HW, F_, F_, w1t, b1, w2t, b2)
+    ref = head_ref(x, B, HW, F_, F_, w1, b1, w2, b2)
     assert torch.allclose(out, ref, atol=1e-4, rtol=1e-3), (out - ref).abs().max()

@@ -1,0 +1,80 @@
+#!/usr/bin/env python
+"""Per-kernel micro-benchmark on the GPU: time every tile config of the fused
+conv-GEMM on Xception layer shapes (random data, interleaved rounds in one
+process, cdna guide §5.4 rule 24)."""
+from __future__ import annotations
+
+import argparse
+import statistics
+
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+
+from kdl.ops import _lib
+from kdl.ops.conv import MODE_DW, MODE_PW, MODE_CONV, Geometry, cfg_tile
+
+SHAPES = {
+    # name: (mode, cin, n, H, stride)
+    "mid_sep": (MODE_DW, 728, 728, 19, 1),
+    "mid_pw": (MODE_PW, 728, 728, 19, 1),
+    "b2_sep2": (MODE_DW, 128, 128, 147, 1),
+    "b2_sep1": (MODE_DW, 64, 128, 147, 1),
+    "b4_sep2": (MODE_DW, 728, 728, 37, 1),
+    "b14_sep2": (MODE_DW, 1536, 2048, 10, 1),
+    "stem2": (MODE_CONV, 32, 64, 149, 1),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    a = ap.parse_args()
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+    from test_kernels_gpu import _layer, _rand_act  # reuse the test constructors
+    gen = torch.Generator().manual_seed(0)
+    C = _lib.lib()
+    s = torch.cuda.current_stream()
+    for name in a.shapes.split(","):
+        mode, cin, n, H, stride = SHAPES[name]
+        lay = _layer(mode, cin, n, gen, stride=stride, relu_in=mode == MODE_DW)
+        B = a.batch
+        if mode == MODE_CONV:
+            g = Geometry(B, H, H, H - 2, H - 2)
+        elif mode == MODE_PW:
+            oh = (H - 1) // stride + 1
+            g = Geometry(B, H, H, oh, oh)
+        else:
+            g = Geometry(B, H, H, H, H)
+        x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
+        y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device="cuda")
+        macs = g.M * n * (9 * cin if mode == MODE_CONV else cin)
+        tmp = torch.zeros(g.M * lay.cin_pad, dtype=torch.bfloat16, device="cuda")
+        times = {v: [] for v in lay.variants()}
+        for _ in range(a.rounds):
+            for split, cfg in lay.variants():
+                def run():
+                    lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, tmp=_lib.ptr(tmp), split=split, cfg=cfg)
+                run()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    run()
+                e1.record()
+                e1.synchronize()
+                times[(split, cfg)].append(e0.elapsed_time(e1) / a.iters * 1e3)
+        print(f"== {name}: M={g.M} K={lay.K} N={n} ({macs / 1e9:.2f} GMAC)")
+        for (split, cfg), ts in sorted(times.items(), key=lambda kv: min(kv[1]))[:6]:
+            t = statistics.median(ts)
+            print(f"   {'split' if split else 'fused'} cfg {cfg:2d} tile {cfg_tile(cfg)}: {t:8.1f} us  "
+                  f"{2 * macs / t / 1e6:7.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
