@@ -296,6 +296,8 @@ static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (a.K % 32 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (cfg >= SEP_CFG_BASE) return mode == MODE_DW ? sepconv_fused(cfg - SEP_CFG_BASE, a, s) : hipErrorInvalidValue;
+  if (cfg >= PIPE_CFG_BASE) return gemm_pipe(mode, cfg - PIPE_CFG_BASE, a, s);
   switch (mode) {
     case MODE_PW: return launch_mode<MODE_PW>(cfg, a, s);
     case MODE_CONV: return launch_mode<MODE_CONV>(cfg, a, s);
@@ -305,6 +307,8 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
 }
 
 int conv_gemm_config(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg >= SEP_CFG_BASE) return sepconv_fused_config(cfg - SEP_CFG_BASE, bm, bn, threads);
+  if (cfg >= PIPE_CFG_BASE) return gemm_pipe_config(cfg - PIPE_CFG_BASE, bm, bn, threads);
   switch (cfg) {
 #define KDL_INFO(id, fm, fn, wgm, wgn) \
   case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;

@@ -1,0 +1,243 @@
+// Pipelined conv-GEMM for the pointwise (MODE_PW) and implicit-3x3 (MODE_CONV)
+// lowerings: Y[m][n] = sum_k A[m][k] W[n][k] + bias (+ReLU)(+residual), bf16 NHWC.
+//
+// CDNA4 structure (cdna_hip_programming.md §5, "Pipelining across barriers"):
+//   * BOTH operands are staged global->LDS by LDS-DMA (global_load_lds_dwordx4);
+//     no VGPR-destination loads in the k-loop, so hipcc never inserts a draining
+//     vmcnt(0) (guide §5 trap (b): "go all-glds for both operands").
+//   * a STAGES-deep LDS ring; stage t+STAGES-1 is issued while stage t is
+//     consumed, and the wait before each barrier is a COUNTED vmcnt that leaves
+//     the younger stages in flight across the raw s_barrier.
+//   * one barrier per 32-deep k-step; MFMA v_mfma_f32_16x16x32_bf16 with swapped
+//     operands so each lane's accumulator holds 4 consecutive output channels
+//     (8-byte LDS writes in the epilogue, 16-byte coalesced global stores).
+//   * fragment-linear LDS image (1 KiB per 16x32 fragment, lane l at l*16): what
+//     one LDS-DMA wave instruction writes is exactly what ds_read_b128 of the MFMA
+//     operand reads -> conflict-free without a swizzle.
+//   * XCD-aware bijective block remap (T1).
+#include "common.h"
+#include "launch.h"
+
+namespace kdl {
+
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int BM = 16 * FM * WGM;
+  constexpr int BN = 16 * FN * WGN;
+  constexpr int AF = BM / 16, BF = BN / 16;
+  constexpr int FR = AF + BF;                 // 1 KiB fragments per stage
+  // LDS-DMA instructions per wave per stage. When FR does not split evenly, the
+  // surplus slots re-issue the last fragment (identical bytes to the identical
+  // LDS slot), so every wave issues exactly L and one counted vmcnt fits all.
+  constexpr int L = (FR + NW - 1) / NW;
+  constexpr int STAGE = FR * 1024 * KSUB;     // KSUB 32-deep k sub-steps per stage
+  constexpr int CS = BN * 2 + 16;
+  constexpr int SMEM_PIPE = STAGES * STAGE;
+  constexpr int SMEM_C = BM * CS;
+  constexpr int SMEM = SMEM_PIPE > SMEM_C ? SMEM_PIPE : SMEM_C;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int nN = (a.NF * 16) / BN;
+  const int nM = (a.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, nM * nN);
+  const int mi = wg / nN, ni = wg % nN;
+  const int m0 = mi * BM, n0 = ni * BN;
+  const int KT32 = a.K >> 5;                  // 32-deep k steps
+  const int KT = (KT32 + KSUB - 1) / KSUB;    // pipeline stages
+  const int OHW = a.OH * a.OW;
+
+  // per-lane source offsets of the fragments this wave stages
+  long src[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int f = min(wave + i * NW, FR - 1);
+    if (f < AF) {
+      int m = m0 + f * 16 + (lane & 15);
+      m = m < a.M ? m : a.M - 1;
+      const int b = m / OHW, rem = m - b * OHW;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      long pix;
+      if constexpr (MODE == 0)
+        pix = ((long)b * a.H + (long)oh * a.stride) * a.W + (long)ow * a.stride;
+      else
+        pix = ((long)b * a.H + oh) * a.W + ow;
+      src[i] = pix * a.ldx + 8 * (lane >> 4);
+    } else {
+      const int nf = n0 / 16 + (f - AF);
+      src[i] = ((long)nf * KT32) * 512 + lane * 8;
+    }
+  }
+
+  // Issue stage t (k32 steps t*KSUB .. t*KSUB+KSUB-1). A sub-step past the end
+  // of K re-issues the stage's first sub-step into its own slot (its MFMAs are
+  // skipped), so every stage has exactly L*KSUB DMAs for the counted vmcnt.
+  auto issue = [&](int t, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < KSUB; ++ks) {
+      int k32 = t * KSUB + ks;
+      if (k32 >= KT32) k32 = t * KSUB;
+      long koff_a;
+      if constexpr (MODE == 0) {
+        koff_a = (long)k32 * 32;
+      } else {
+        const int k = k32 * 32;
+        const int tap = k / a.cin, c0 = k - tap * a.cin;
+        koff_a = ((long)(tap / 3) * a.W + (tap % 3)) * a.ldx + c0;
+      }
+      uint8_t* base = smem + buf * STAGE + ks * FR * 1024;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const int f = min(wave + i * NW, FR - 1);
+        if (f < AF) glds16(a.x + src[i] + koff_a, base + f * 1024);
+        else glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < KT) issue(p, p);
+
+  for (int t = 0; t < KT; ++t) {
+    // stages issued after t so far: min(KT-1, t+STAGES-2) - t
+    const int after = min(KT - 1, t + STAGES - 2) - t;
+    if (after >= 2) wait_vm_barrier<2 * L * KSUB>();
+    else if (after == 1) wait_vm_barrier<L * KSUB>();
+    else wait_vm_barrier<0>();
+    if (t + STAGES - 1 < KT) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+#pragma unroll
+    for (int ks = 0; ks < KSUB; ++ks) {
+      if (KSUB > 1 && t * KSUB + ks >= KT32) break;
+      const uint8_t* st = smem + (t % STAGES) * STAGE + ks * FR * 1024 + lane * 16;
+      s16x8 af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+    }
+  }
+  wait_vm_barrier<0>();
+
+  // epilogue: bias + ReLU -> bf16 C tile in LDS -> (+residual) 16-byte stores
+  const int quad = lane >> 4, col = lane & 15;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nl = wn * FN * 16 + j * 16 + 4 * quad;
+    const float4 bv = *(const float4*)(a.bias + n0 + nl);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = wm * FM * 16 + i * 16 + col;
+      float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y;
+      float v2 = acc[i][j][2] + bv.z, v3 = acc[i][j][3] + bv.w;
+      if (a.relu_out) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int c = tid; c < BM * CPR; c += 64 * NW) {
+    const int r = c / CPR, cc = c - r * CPR;
+    const int m = m0 + r, n = n0 + cc * 8;
+    if (m < a.M && n < a.nstore) {
+      u32x4 v = *(const u32x4*)(smem + r * CS + cc * 16);
+      if (a.res) {
+        const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
+      }
+      *(u32x4*)(a.y + (long)m * a.ldy + n) = v;
+    }
+  }
+}
+
+// (FM, FN, WGM, WGN, STAGES); ids are offset by PIPE_CFG_BASE in the host table.
+#define KDL_PIPE_CONFIGS(X) \
+  X(0, 4, 4, 2, 2, 4, 1)    \
+  X(1, 2, 4, 2, 2, 4, 1)    \
+  X(2, 4, 2, 2, 2, 4, 1)    \
+  X(3, 2, 2, 2, 2, 4, 1)    \
+  X(4, 8, 2, 1, 4, 4, 1)    \
+  X(5, 4, 4, 1, 4, 4, 1)    \
+  X(6, 4, 8, 2, 2, 3, 1)    \
+  X(7, 8, 4, 1, 4, 3, 1)    \
+  X(8, 3, 6, 2, 4, 3, 1)    \
+  X(9, 6, 3, 2, 4, 3, 1)    \
+  X(10, 3, 3, 2, 4, 3, 1)   \
+  X(11, 4, 4, 2, 2, 3, 1)   \
+  X(12, 2, 6, 2, 4, 3, 1)   \
+  X(13, 4, 2, 2, 4, 3, 1)   \
+  X(14, 3, 3, 2, 4, 2, 2)   \
+  X(15, 6, 3, 2, 4, 2, 2)   \
+  X(16, 4, 2, 2, 4, 2, 2)   \
+  X(17, 4, 4, 2, 2, 3, 2)   \
+  X(18, 3, 3, 2, 4, 3, 2)   \
+  X(19, 4, 4, 2, 2, 2, 4)   \
+  X(20, 2, 4, 2, 2, 3, 2)   \
+  X(21, 4, 2, 2, 2, 3, 2)   \
+  X(22, 6, 3, 2, 4, 5, 1)   \
+  X(23, 3, 6, 2, 4, 5, 1)   \
+  X(24, 3, 3, 2, 4, 6, 1)   \
+  X(25, 4, 2, 2, 4, 6, 1)   \
+  X(26, 6, 3, 2, 4, 3, 2)
+
+template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS>
+static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
+  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
+  if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
+  const int nM = (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS>), dim3(nM * nN), dim3(64 * WGM * WGN), 0,
+                     s, a);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
+  switch (cfg) {
+#define KDL_PCASE(id, fm, fn, wgm, wgn, st, ks) \
+  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks>(a, s);
+    KDL_PIPE_CONFIGS(KDL_PCASE)
+#undef KDL_PCASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
+  if (a.K % 32 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (mode == 0) return launch_pipe_mode<0>(cfg, a, s);
+  if (mode == 1) return launch_pipe_mode<1>(cfg, a, s);
+  return hipErrorInvalidValue;
+}
+
+int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads) {
+  switch (cfg) {
+#define KDL_PINFO(id, fm, fn, wgm, wgn, st, ks) \
+  case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
+    KDL_PIPE_CONFIGS(KDL_PINFO)
+#undef KDL_PINFO
+    default: return -1;
+  }
+}
+
+}  // namespace kdl

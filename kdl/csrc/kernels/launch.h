@@ -26,7 +26,16 @@ struct ConvGemmArgs {
   int relu_in, relu_out;
 };
 
+// cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
+// cfg >= PIPE_CFG_BASE: LDS-DMA pipelined kernel (MODE_PW / MODE_CONV only).
+constexpr int PIPE_CFG_BASE = 16;
+// cfg >= SEP_CFG_BASE: fused separable conv (MODE_DW only, sepconv_fused.hip).
+constexpr int SEP_CFG_BASE = 64;
+hipError_t sepconv_fused(int cfg, const ConvGemmArgs& a, hipStream_t s);
+int sepconv_fused_config(int cfg, int* bm, int* bn, int* threads);
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
+hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
+int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads);
 int conv_gemm_config(int cfg, int* bm, int* bn, int* threads);
 int conv_gemm_num_configs();
 

@@ -276,7 +276,7 @@ class XceptionEngine:
                 x, y = self.bufs[step.src], self.bufs[step.dst]
                 res = self.bufs[step.res] if step.res else None
                 best = None
-                for split, cfg in lay.variants():
+                for split, cfg in lay.variants(W):
                     def run():
                         lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res),
                                  ldx=self.shapes[step.src][2],

@@ -17,9 +17,40 @@ from .pack import pack_fragments, pad_vec, round_up
 
 MODE_PW, MODE_CONV, MODE_DW = 0, 1, 2
 
-# (FM, FN, WGM, WGN) — keep in sync with KDL_CONFIGS in conv_gemm.hip
-CONFIGS = [(2, 2, 2, 2), (4, 2, 2, 2), (2, 4, 2, 2), (4, 4, 2, 2), (4, 6, 1, 8),
-           (2, 12, 1, 4), (4, 4, 1, 4), (2, 6, 1, 8), (8, 2, 1, 4), (4, 2, 1, 4)]
+# (FM, FN, WGM, WGN): block tile = (16*FM*WGM) x (16*FN*WGN).
+# ids < PIPE_BASE: KDL_CONFIGS in conv_gemm.hip (register-B kernel, supports the
+# fused depthwise producer); ids >= PIPE_BASE: KDL_PIPE_CONFIGS in gemm_pipe.hip
+# (LDS-DMA ring, pointwise / 3x3 only).
+PIPE_BASE = 16
+CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4: (4, 6, 1, 8),
+           5: (2, 12, 1, 4), 6: (4, 4, 1, 4), 7: (2, 6, 1, 8), 8: (8, 2, 1, 4), 9: (4, 2, 1, 4),
+           16: (4, 4, 2, 2), 17: (2, 4, 2, 2), 18: (4, 2, 2, 2), 19: (2, 2, 2, 2),
+           20: (8, 2, 1, 4), 21: (4, 4, 1, 4), 22: (4, 8, 2, 2), 23: (8, 4, 1, 4),
+           24: (3, 6, 2, 4), 25: (6, 3, 2, 4), 26: (3, 3, 2, 4), 27: (4, 4, 2, 2),
+           28: (2, 6, 2, 4), 29: (4, 2, 2, 4), 30: (3, 3, 2, 4), 31: (6, 3, 2, 4),
+           32: (4, 2, 2, 4), 33: (4, 4, 2, 2), 34: (3, 3, 2, 4), 35: (4, 4, 2, 2),
+           36: (2, 4, 2, 2), 37: (4, 2, 2, 2), 38: (6, 3, 2, 4), 39: (3, 6, 2, 4),
+           40: (3, 3, 2, 4), 41: (4, 2, 2, 4), 42: (6, 3, 2, 4),
+           # ids >= SEP_BASE: fused separable conv (sepconv_fused.hip): (FM, NFW, 1, NW)
+           64: (4, 6, 1, 8), 65: (4, 1, 1, 8), 66: (4, 2, 1, 8), 67: (2, 6, 1, 8), 68: (4, 4, 1, 8),
+           69: (4, 3, 1, 8), 70: (8, 1, 1, 8), 71: (8, 2, 1, 8), 72: (2, 3, 1, 8), 73: (4, 2, 1, 4),
+           74: (4, 1, 1, 4)}
+SEP_BASE = 64
+# staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
+SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
+
+
+def config_applicable(cfg: int, W: int | None) -> bool:
+    """Mirror of the host-side launch checks in sepconv_fused.hip."""
+    if cfg < SEP_BASE or W is None:
+        return True
+    fm, nfw, _, nw = CONFIGS[cfg]
+    bm, bn = 16 * fm, 16 * nfw * nw
+    maxr = (bm - 1) // W + 4
+    if maxr * W * 4 > SEP_SPT[cfg] * 64 * nw:
+        return False
+    pipe = 2 * maxr * W * 64 + 2 * bm * 64 + 2 * 288 * 4
+    return max(pipe, bm * (bn * 2 + 16)) <= 160 * 1024
 
 
 def cfg_tile(cfg: int) -> tuple[int, int]:
@@ -29,16 +60,18 @@ def cfg_tile(cfg: int) -> tuple[int, int]:
 
 def candidate_configs(n: int, m: int | None = None) -> list[int]:
     """Configs whose N tile does not waste more than ~35% of the channels."""
-    out = [c for c in range(len(CONFIGS)) if round_up(n, cfg_tile(c)[1]) <= 1.35 * round_up(n, 16)]
+    ids = sorted(CONFIGS)
+    out = [c for c in ids if round_up(n, cfg_tile(c)[1]) <= 1.35 * round_up(n, 16)]
     if not out:  # tiny N: smallest N tile only
-        bn_min = min(cfg_tile(c)[1] for c in range(len(CONFIGS)))
-        out = [c for c in range(len(CONFIGS)) if cfg_tile(c)[1] == bn_min]
+        bn_min = min(cfg_tile(c)[1] for c in ids)
+        out = [c for c in ids if cfg_tile(c)[1] == bn_min]
     return out
 
 
 def default_config(mode: int, n: int, m: int) -> int:
     cands = candidate_configs(n, m)
-    pref = [4, 6, 3, 2, 1, 0] if mode == MODE_DW else [3, 6, 1, 2, 0]
+    pref = [4, 6, 3, 2, 1, 0] if mode == MODE_DW else [16, 21, 18, 17, 19, 3, 6, 1, 2, 0]
+    # (fused-separable ids are picked by the autotuner, which knows the image width)
     for c in pref:
         if c in cands:
             return c
@@ -93,11 +126,14 @@ class ConvGemmLayer:
         # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
         self.split = False
 
-    def variants(self) -> list[tuple[bool, int]]:
-        v = [(False, c) for c in self.candidates]
-        if self.mode == MODE_DW:
-            v += [(True, c) for c in self.candidates]
-        return v
+    def variants(self, W: int | None = None) -> list[tuple[bool, int]]:
+        """(split, cfg) pairs valid for this layer (``W``: image width, filters the
+        fused separable configs whose LDS row band would not fit)."""
+        if self.mode != MODE_DW:
+            return [(False, c) for c in self.candidates if c < SEP_BASE]
+        return ([(False, c) for c in self.candidates
+                 if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W)]
+                + [(True, c) for c in self.candidates if c < SEP_BASE])
 
     def dw_args(self, x: int, tmp: int, g: Geometry, ldx: int | None = None) -> dict:
         assert (ldx or self.cin_pad) == self.cin_pad

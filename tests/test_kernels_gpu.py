@@ -60,7 +60,7 @@ def test_conv_gemm_pointwise(cin, n, H, stride):
     g = Geometry(B, H, H, OH, OH)
     x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
     ref = conv_gemm_ref(lay, x, g)
-    for cfg in lay.candidates:
+    for _, cfg in lay.variants(H):
         y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
         lay.launch(x, y, g, cfg=cfg)
         torch.cuda.synchronize()
@@ -74,7 +74,7 @@ def test_conv_gemm_conv3x3():
     g = Geometry(B, H, H, H - 2, H - 2)
     x = _rand_act((B, H, H), 32, 32, gen)
     ref = conv_gemm_ref(lay, x, g)
-    for cfg in lay.candidates:
+    for _, cfg in lay.variants(H):
         y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
         lay.launch(x, y, g, cfg=cfg)
         torch.cuda.synchronize()
@@ -96,7 +96,7 @@ def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
     x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
     res = _rand_act((B, H, H), lay.ldy, n, gen) if with_res else None
     ref = conv_gemm_ref(lay, x, g, res=res)
-    for split, cfg in lay.variants():
+    for split, cfg in lay.variants(H):
         y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
         lay.launch(x, y, g, res=res, cfg=cfg, split=split)
         torch.cuda.synchronize()
@@ -110,7 +110,7 @@ def test_conv_gemm_repeat_race_screen():
     B, H = 8, 19
     g = Geometry(B, H, H, H, H)
     x = _rand_act((B, H, H), lay.cin_pad, 728, gen)
-    for split, cfg in lay.variants():
+    for split, cfg in lay.variants(H):
         y0 = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
         lay.launch(x, y0, g, cfg=cfg, split=split)
         for _ in range(10):

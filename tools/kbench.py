@@ -25,6 +25,10 @@ SHAPES = {
     "b4_sep2": (MODE_DW, 728, 728, 37, 1),
     "b14_sep2": (MODE_DW, 1536, 2048, 10, 1),
     "stem2": (MODE_CONV, 32, 64, 149, 1),
+    # ablations of the middle-flow GEMM: K x2 / x0.5, M x2 (via --batch)
+    "mid_pw_k2": (MODE_PW, 1456, 728, 19, 1),
+    "mid_pw_kh": (MODE_PW, 352, 728, 19, 1),
+    "mid_pw_n2": (MODE_PW, 728, 1456, 19, 1),
 }
 
 
@@ -34,6 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--top", type=int, default=6)
     a = ap.parse_args()
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
@@ -56,9 +61,9 @@ def main():
         y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device="cuda")
         macs = g.M * n * (9 * cin if mode == MODE_CONV else cin)
         tmp = torch.zeros(g.M * lay.cin_pad, dtype=torch.bfloat16, device="cuda")
-        times = {v: [] for v in lay.variants()}
+        times = {v: [] for v in lay.variants(H)}
         for _ in range(a.rounds):
-            for split, cfg in lay.variants():
+            for split, cfg in lay.variants(H):
                 def run():
                     lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, tmp=_lib.ptr(tmp), split=split, cfg=cfg)
                 run()
@@ -70,7 +75,7 @@ def main():
                 e1.synchronize()
                 times[(split, cfg)].append(e0.elapsed_time(e1) / a.iters * 1e3)
         print(f"== {name}: M={g.M} K={lay.K} N={n} ({macs / 1e9:.2f} GMAC)")
-        for (split, cfg), ts in sorted(times.items(), key=lambda kv: min(kv[1]))[:6]:
+        for (split, cfg), ts in sorted(times.items(), key=lambda kv: min(kv[1]))[:a.top]:
             t = statistics.median(ts)
             print(f"   {'split' if split else 'fused'} cfg {cfg:2d} tile {cfg_tile(cfg)}: {t:8.1f} us  "
                   f"{2 * macs / t / 1e6:7.1f} TF/s")
