@@ -1,0 +1,178 @@
+// pybind11 bindings of the CPU-only native runtime (module kdl._rt): dynamic
+// batcher, TF-Serving Predict wire codec, TensorBundle SSTable reader.
+// Every blocking call releases the GIL so gRPC handler threads and the per-GPU
+// executor threads run truly concurrently.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <fstream>
+#include <sstream>
+
+#include "runtime/batcher.h"
+#include "runtime/sstable.h"
+#include "runtime/tfproto.h"
+
+namespace py = pybind11;
+using namespace kdl;
+
+namespace {
+
+py::dict spec_dict(const ModelSpecView& s) {
+  py::dict d;
+  d["name"] = s.name;
+  d["signature_name"] = s.signature_name;
+  d["version_label"] = s.version_label;
+  d["version"] = s.version;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_rt, m) {
+  m.doc() = "kdl native CPU runtime: dynamic batcher, TF-Serving wire codec, TensorBundle reader";
+  m.def("now_us", &now_us);
+
+  py::register_exception<ProtoError>(m, "ProtoError", PyExc_ValueError);
+
+  m.def("parse_predict_request", [](py::bytes req) {
+    std::string_view sv = req;  // zero-copy view of the Python bytes
+    PredictRequestView v;
+    {
+      py::gil_scoped_release nogil;
+      v = parse_predict_request(reinterpret_cast<const uint8_t*>(sv.data()), sv.size());
+    }
+    py::dict out;
+    out["model_spec"] = spec_dict(v.spec);
+    py::list inputs;
+    for (auto& kv : v.inputs) {
+      const TensorView& t = kv.second;
+      py::dict td;
+      td["key"] = kv.first;
+      td["dtype"] = t.dtype;
+      td["dims"] = t.dims;
+      td["unknown_rank"] = t.unknown_rank;
+      td["has_content"] = t.has_content;
+      td["values_field"] = t.values_field;
+      td["offset"] = t.content_offset;
+      td["size"] = t.content_size;
+      td["unpacked"] = py::bytes(reinterpret_cast<const char*>(t.unpacked.data()), t.unpacked.size());
+      inputs.append(td);
+    }
+    out["inputs"] = inputs;
+    out["output_filter"] = v.output_filter;
+    return out;
+  });
+  m.def("parse_model_spec_request", [](py::bytes req) {
+    std::string_view sv = req;
+    return spec_dict(parse_model_spec_request(reinterpret_cast<const uint8_t*>(sv.data()), sv.size()));
+  });
+  m.def("build_predict_response",
+        [](py::list outputs, const std::string& name, int64_t version, const std::string& signature) {
+          std::vector<OutputTensor> outs;
+          std::vector<py::array_t<float, py::array::c_style | py::array::forcecast>> keep;
+          for (auto item : outputs) {
+            auto tup = item.cast<py::tuple>();
+            auto arr = tup[1].cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+            keep.push_back(arr);
+            OutputTensor o;
+            o.key = tup[0].cast<std::string>();
+            for (py::ssize_t i = 0; i < arr.ndim(); ++i) o.dims.push_back(arr.shape(i));
+            o.values = arr.data();
+            outs.push_back(o);
+          }
+          ModelSpecView s;
+          s.name = name;
+          s.version = version;
+          s.signature_name = signature;
+          std::string b = build_predict_response(outs, s);
+          return py::bytes(b);
+        });
+
+  m.def("crc32c", [](py::bytes b, uint32_t init) {
+    std::string_view sv = b;
+    return crc32c(reinterpret_cast<const uint8_t*>(sv.data()), sv.size(), init);
+  }, py::arg("data"), py::arg("init") = 0);
+  m.def("crc32c_unmask", &crc32c_unmask);
+  m.def("snappy_uncompress", [](py::bytes b) {
+    std::string_view sv = b;
+    return py::bytes(snappy_uncompress(reinterpret_cast<const uint8_t*>(sv.data()), sv.size()));
+  });
+  m.def("read_sstable", [](py::bytes data, bool verify) {
+    std::string file = data;
+    std::vector<std::pair<std::string, std::string>> kv;
+    {
+      py::gil_scoped_release nogil;
+      kv = read_sstable(file, verify);
+    }
+    py::list out;
+    for (auto& e : kv) out.append(py::make_tuple(py::bytes(e.first), py::bytes(e.second)));
+    return out;
+  }, py::arg("data"), py::arg("verify_crc") = true);
+
+  py::class_<Batch>(m, "Batch")
+      .def_readonly("id", &Batch::id)
+      .def_readonly("n_real", &Batch::n_real)
+      .def_readonly("bucket", &Batch::bucket)
+      .def_readonly("tickets", &Batch::tickets)
+      .def_readonly("first_item", &Batch::first_item)
+      .def_readonly("n_items", &Batch::n_items)
+      .def_readonly("oldest_enqueue_us", &Batch::oldest_enqueue_us);
+
+  py::class_<DynamicBatcher>(m, "DynamicBatcher")
+      .def(py::init([](int max_batch_size, int64_t batch_timeout_us, int max_enqueued_batches,
+                       std::vector<int> allowed_batch_sizes, size_t item_bytes, int out_cols) {
+             BatcherOptions o;
+             o.max_batch_size = max_batch_size;
+             o.batch_timeout_us = batch_timeout_us;
+             o.max_enqueued_batches = max_enqueued_batches;
+             o.allowed_batch_sizes = allowed_batch_sizes;
+             o.item_bytes = item_bytes;
+             o.out_cols = out_cols;
+             return new DynamicBatcher(o);
+           }),
+           py::arg("max_batch_size") = 32, py::arg("batch_timeout_us") = 2000,
+           py::arg("max_enqueued_batches") = 1000, py::arg("allowed_batch_sizes") = std::vector<int>{},
+           py::arg("item_bytes") = 0, py::arg("out_cols") = 0)
+      // `data` must stay alive until wait() returns (the Python wrapper holds it).
+      .def("submit", [](DynamicBatcher& b, py::buffer data, int n_items, int64_t deadline_us) {
+        py::buffer_info info = data.request();
+        const size_t need = size_t(n_items) * b.options().item_bytes;
+        if (size_t(info.size) * size_t(info.itemsize) < need) throw std::invalid_argument("payload smaller than n_items*item_bytes");
+        return b.submit(reinterpret_cast<const uint8_t*>(info.ptr), n_items, deadline_us);
+      })
+      .def("wait", [](DynamicBatcher& b, int64_t ticket, py::array_t<float, py::array::c_style> out) {
+        float* p = out.mutable_data();
+        py::gil_scoped_release nogil;
+        return b.wait(ticket, p);
+      })
+      .def("next_batch", [](DynamicBatcher& b, uintptr_t staging, int64_t poll_us) -> py::object {
+        Batch batch;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = b.next_batch(reinterpret_cast<uint8_t*>(staging), poll_us, &batch);
+        }
+        if (!ok) return py::none();
+        return py::cast(batch);
+      })
+      .def("finish", [](DynamicBatcher& b, const Batch& batch, uintptr_t results, int status) {
+        py::gil_scoped_release nogil;
+        b.finish(batch, reinterpret_cast<const float*>(results), status);
+      })
+      .def("bucket_for", &DynamicBatcher::bucket_for)
+      .def("shutdown", &DynamicBatcher::shutdown)
+      .def("stats", [](const DynamicBatcher& b) {
+        BatcherStats s = b.stats();
+        py::dict d;
+        d["submitted"] = s.submitted; d["completed"] = s.completed; d["expired"] = s.expired;
+        d["rejected"] = s.rejected; d["batches"] = s.batches; d["items"] = s.items;
+        d["padded_items"] = s.padded_items; d["queue_items"] = s.queue_items;
+        return d;
+      });
+  m.attr("ST_OK") = int(ST_OK);
+  m.attr("ST_DEADLINE") = int(ST_DEADLINE);
+  m.attr("ST_SHUTDOWN") = int(ST_SHUTDOWN);
+  m.attr("ST_ERROR") = int(ST_ERROR);
+  m.attr("ST_QUEUE_FULL") = int(ST_QUEUE_FULL);
+}

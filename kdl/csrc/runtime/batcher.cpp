@@ -1,0 +1,192 @@
+#include "batcher.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace kdl {
+
+int64_t now_us() {
+  return std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+DynamicBatcher::DynamicBatcher(const BatcherOptions& o) : opt_(o) {
+  std::sort(opt_.allowed_batch_sizes.begin(), opt_.allowed_batch_sizes.end());
+  if (!opt_.allowed_batch_sizes.empty() && opt_.allowed_batch_sizes.back() != opt_.max_batch_size)
+    opt_.allowed_batch_sizes.push_back(opt_.max_batch_size);  // TF-Serving requires last == max
+}
+
+DynamicBatcher::~DynamicBatcher() { shutdown(); }
+
+int DynamicBatcher::bucket_for(int n) const {
+  for (int b : opt_.allowed_batch_sizes)
+    if (b >= n) return b;
+  return n;
+}
+
+int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadline_us) {
+  if (n_items <= 0 || n_items > opt_.max_batch_size) return -ST_ERROR;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (shutdown_) return -ST_SHUTDOWN;
+  if (queued_items_ + n_items > int64_t(opt_.max_enqueued_batches) * opt_.max_batch_size) {
+    ++st_.rejected;
+    return -ST_QUEUE_FULL;
+  }
+  auto r = std::make_shared<Req>();
+  r->ticket = next_ticket_++;
+  r->data = data;
+  r->n_items = n_items;
+  r->enqueue_us = now_us();
+  r->deadline_us = deadline_us;
+  queue_.push_back(r);
+  live_[r->ticket] = r;
+  queued_items_ += n_items;
+  ++st_.submitted;
+  cv_consumer_.notify_one();
+  return r->ticket;
+}
+
+int DynamicBatcher::wait(int64_t ticket, float* out) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = live_.find(ticket);
+  if (it == live_.end()) return ST_ERROR;
+  auto r = it->second;
+  for (;;) {
+    if (r->state == DONE || r->state == ABANDONED) break;   // ABANDONED: expired by next_batch
+    if (shutdown_ && r->state != TAKEN) {   // TAKEN: payload copy in flight, wait for it
+      if (r->state == QUEUED) {
+        auto q = std::find(queue_.begin(), queue_.end(), r);
+        if (q != queue_.end()) { queue_.erase(q); queued_items_ -= r->n_items; }
+      }
+      r->state = ABANDONED;
+      r->status = ST_SHUTDOWN;
+      break;
+    }
+    const int64_t now = now_us();
+    if (r->deadline_us > 0 && now >= r->deadline_us && r->state != TAKEN) {
+      // expired: a QUEUED request is removed here; a COPIED one is abandoned
+      // (its payload is no longer referenced, finish() will skip it)
+      if (r->state == QUEUED) {
+        auto q = std::find(queue_.begin(), queue_.end(), r);
+        if (q != queue_.end()) { queue_.erase(q); queued_items_ -= r->n_items; }
+      }
+      r->state = ABANDONED;
+      r->status = ST_DEADLINE;
+      ++st_.expired;
+      break;
+    }
+    if (r->deadline_us > 0 && r->state != TAKEN)
+      cv_producer_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, r->deadline_us - now)));
+    else
+      cv_producer_.wait(lk);
+  }
+  const int status = r->status;
+  if (status == ST_OK && out) std::memcpy(out, r->result.data(), r->result.size() * sizeof(float));
+  live_.erase(ticket);
+  return status;
+}
+
+bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b) {
+  std::vector<std::shared_ptr<Req>> take;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    const int64_t give_up = now_us() + poll_us;
+    for (;;) {
+      if (shutdown_) return false;
+      // drop expired requests at the head of the queue
+      const int64_t now = now_us();
+      for (auto q = queue_.begin(); q != queue_.end();) {
+        if ((*q)->deadline_us > 0 && now >= (*q)->deadline_us) {
+          (*q)->state = ABANDONED;
+          (*q)->status = ST_DEADLINE;
+          queued_items_ -= (*q)->n_items;
+          ++st_.expired;
+          q = queue_.erase(q);
+          cv_producer_.notify_all();
+        } else {
+          ++q;
+        }
+      }
+      if (!queue_.empty()) {
+        const bool full = queued_items_ >= opt_.max_batch_size;
+        const bool timed_out = now - queue_.front()->enqueue_us >= opt_.batch_timeout_us;
+        if (full || timed_out) break;
+        const int64_t wake = std::min(give_up, queue_.front()->enqueue_us + opt_.batch_timeout_us);
+        if (now >= give_up) return false;
+        cv_consumer_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));
+      } else {
+        if (now >= give_up) return false;
+        cv_consumer_.wait_for(lk, std::chrono::microseconds(give_up - now));
+      }
+    }
+    // greedily pack whole requests in FIFO order
+    int n = 0;
+    b->tickets.clear(); b->first_item.clear(); b->n_items.clear();
+    b->oldest_enqueue_us = queue_.front()->enqueue_us;
+    while (!queue_.empty() && n + queue_.front()->n_items <= opt_.max_batch_size) {
+      auto r = queue_.front();
+      queue_.pop_front();
+      queued_items_ -= r->n_items;
+      r->state = TAKEN;
+      b->tickets.push_back(r->ticket);
+      b->first_item.push_back(n);
+      b->n_items.push_back(r->n_items);
+      n += r->n_items;
+      take.push_back(r);
+    }
+    b->id = next_batch_++;
+    b->n_real = n;
+    b->bucket = bucket_for(n);
+    ++st_.batches;
+    st_.items += n;
+    st_.padded_items += b->bucket - n;
+  }
+  // payload copies outside the lock (producers stay blocked in wait() on TAKEN)
+  if (staging && opt_.item_bytes) {
+    for (size_t i = 0; i < take.size(); ++i)
+      std::memcpy(staging + size_t(b->first_item[i]) * opt_.item_bytes, take[i]->data,
+                  size_t(take[i]->n_items) * opt_.item_bytes);
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& r : take)
+      if (r->state == TAKEN) r->state = COPIED;
+  }
+  cv_producer_.notify_all();
+  return true;
+}
+
+void DynamicBatcher::finish(const Batch& b, const float* results, int status) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (size_t i = 0; i < b.tickets.size(); ++i) {
+    auto it = live_.find(b.tickets[i]);
+    if (it == live_.end()) continue;
+    auto& r = it->second;
+    if (r->state == ABANDONED) continue;
+    r->status = status;
+    if (status == ST_OK && results) {
+      const size_t n = size_t(b.n_items[i]) * opt_.out_cols;
+      r->result.assign(results + size_t(b.first_item[i]) * opt_.out_cols,
+                       results + size_t(b.first_item[i]) * opt_.out_cols + n);
+    }
+    r->state = DONE;
+    ++st_.completed;
+  }
+  cv_producer_.notify_all();
+}
+
+void DynamicBatcher::shutdown() {
+  std::lock_guard<std::mutex> lk(mu_);
+  shutdown_ = true;
+  cv_consumer_.notify_all();
+  cv_producer_.notify_all();
+}
+
+BatcherStats DynamicBatcher::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  BatcherStats s = st_;
+  s.queue_items = queued_items_;
+  return s;
+}
+
+}  // namespace kdl

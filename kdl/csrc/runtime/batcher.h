@@ -1,0 +1,98 @@
+// Deadline-aware dynamic batcher (TF-Serving BasicBatchScheduler equivalent,
+// SURVEY.md §2.3 X2 / §2.10 C5, C16).
+//
+// Producers (gRPC / REST handler threads, GIL released) submit requests of
+// n_items fixed-size items and block in wait(). Consumers (one executor thread per
+// GPU) call next_batch(), which forms a batch of up to max_batch_size items once
+// the queue holds a full batch or the oldest request has waited
+// batch_timeout_us, drops requests whose deadline has passed, copies the
+// payloads into the consumer's pinned staging buffer and rounds the batch up to
+// the smallest allowed bucket (one captured hipGraph per bucket). finish()
+// scatters result rows back and wakes the producers.
+//
+// Knobs mirror TF-Serving's --batching_parameters_file: max_batch_size,
+// batch_timeout_micros, max_enqueued_batches, allowed_batch_sizes.
+#pragma once
+#include <stdint.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+namespace kdl {
+
+struct BatcherOptions {
+  int max_batch_size = 32;
+  int64_t batch_timeout_us = 2000;
+  int max_enqueued_batches = 1000;
+  std::vector<int> allowed_batch_sizes;      // sorted ascending; empty = exact batch sizes
+  size_t item_bytes = 0;
+  int out_cols = 0;                          // floats per item result row
+};
+
+enum BatchStatus { ST_OK = 0, ST_DEADLINE = 1, ST_SHUTDOWN = 2, ST_ERROR = 3, ST_PENDING = 4, ST_QUEUE_FULL = 5 };
+
+struct Batch {
+  int64_t id = 0;
+  int n_real = 0;                            // real items
+  int bucket = 0;                            // padded batch size (graph bucket)
+  std::vector<int64_t> tickets;
+  std::vector<int> first_item;               // offset of each ticket's items in the batch
+  std::vector<int> n_items;
+  int64_t oldest_enqueue_us = 0;
+};
+
+struct BatcherStats {
+  int64_t submitted = 0, completed = 0, expired = 0, rejected = 0, batches = 0, items = 0, padded_items = 0;
+  int64_t queue_items = 0;
+};
+
+int64_t now_us();
+
+class DynamicBatcher {
+ public:
+  explicit DynamicBatcher(const BatcherOptions& o);
+  ~DynamicBatcher();
+
+  // Producer: returns a ticket (> 0) or -ST_QUEUE_FULL / -ST_SHUTDOWN / -ST_ERROR.
+  // `data` must stay valid until wait() returns for this ticket.
+  int64_t submit(const uint8_t* data, int n_items, int64_t deadline_us);
+  // Blocks until the request completes or its deadline passes; copies
+  // n_items*out_cols floats into `out`. Returns a BatchStatus.
+  int wait(int64_t ticket, float* out);
+
+  // Consumer: waits up to poll_us for a batch; false on timeout/shutdown.
+  bool next_batch(uint8_t* staging, int64_t poll_us, Batch* b);
+  void finish(const Batch& b, const float* results, int status);
+
+  void shutdown();
+  BatcherStats stats() const;
+  int bucket_for(int n) const;
+  const BatcherOptions& options() const { return opt_; }
+
+ private:
+  enum State { QUEUED, TAKEN, COPIED, DONE, ABANDONED };
+  struct Req {
+    int64_t ticket;
+    const uint8_t* data;
+    int n_items;
+    int64_t enqueue_us, deadline_us;
+    State state = QUEUED;
+    int status = ST_PENDING;
+    std::vector<float> result;
+  };
+  BatcherOptions opt_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_consumer_, cv_producer_;
+  std::deque<std::shared_ptr<Req>> queue_;
+  std::unordered_map<int64_t, std::shared_ptr<Req>> live_;
+  int64_t next_ticket_ = 1, next_batch_ = 1, queued_items_ = 0;
+  bool shutdown_ = false;
+  BatcherStats st_;
+};
+
+}  // namespace kdl

@@ -1,0 +1,318 @@
+"""Servables, signature runners and per-device executors.
+
+Request path: gRPC/REST handler thread -> C++ DynamicBatcher
+(``kdl._rt``; deadline-aware, bucketed) -> one executor thread per device which
+copies the formed batch into pinned staging, H2D, replays the captured
+hipGraph of the bucket, D2H of the logits -> ``finish`` wakes the handlers.
+
+Backends:
+  * ``gpu``: ``kdl.engine.XceptionEngine`` (fused HIP kernels, hipGraph per
+    bucket), one executor per MI355X (data parallel over the node's GPUs: each
+    GPU pulls whole batches from the shared batcher, host-direct H2D over its
+    own PCIe link).
+  * ``cpu``: the fp32 Keras-semantics torch oracle ("config #1: plumbing, no
+    GPU").
+"""
+from __future__ import annotations
+
+import json
+import logging
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from ..models import xception as X
+from ..ops import _lib
+from . import protos as P
+from .config import ServerConfig
+from .metrics import BATCH_BUCKETS, METRICS
+
+log = logging.getLogger("kdl.serving")
+
+IMG = X.INPUT_SIZE
+NATIVE_SIGNATURE = "serving_uint8"     # native fast path: uint8 HWC images (4x fewer bytes)
+NATIVE_INPUT_KEY = "images"
+
+
+class ServingError(Exception):
+    """Carries a gRPC status code name + message (mapped to HTTP on REST)."""
+
+    def __init__(self, code: str, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+@dataclass
+class SignatureInfo:
+    name: str
+    input_key: str
+    input_dtype: int
+    output_key: str
+    method_name: str = "tensorflow/serving/predict"
+    input_shape: tuple = (-1, IMG, IMG, 3)
+    output_shape: tuple = (-1, 10)
+
+
+@dataclass
+class ModelSource:
+    """Where a version's weights come from."""
+    params: dict
+    head: X.Head
+    signatures: dict[str, SignatureInfo] = field(default_factory=dict)
+    origin: str = ""
+
+
+def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
+    """SavedModel (saved_model.pb + variables/), packed kdl safetensors, or synthetic."""
+    path = Path(path)
+    sigs: dict[str, SignatureInfo] = {}
+    if (path / "saved_model.pb").exists():
+        from ..ingest.keras_map import to_xception_params
+        from ..ingest.savedmodel import SavedModelDir
+        sm = SavedModelDir(path)
+        params, head = to_xception_params(sm.variables())
+        for name, s in sm.signatures.items():
+            if not s.inputs or not s.outputs:
+                continue
+            (ik, ispec), = list(s.inputs.items())[:1]
+            (ok, ospec), = list(s.outputs.items())[:1]
+            sigs[name] = SignatureInfo(name, ik, ispec.dtype, ok, s.method_name, ispec.shape, ospec.shape)
+        origin = "saved_model"
+    elif (path / "kdl_params.safetensors").exists():
+        from safetensors.torch import load_file
+        params = load_file(str(path / "kdl_params.safetensors"))
+        meta = json.loads((path / "kdl_model.json").read_text()) if (path / "kdl_model.json").exists() else {}
+        head = X.Head(**meta.get("head", {}))
+        for name, s in meta.get("signatures", {}).items():
+            sigs[name] = SignatureInfo(name=name, input_key=s["input_key"], input_dtype=s.get("input_dtype", 1),
+                                       output_key=s["output_key"])
+        origin = "kdl_safetensors"
+    elif synthetic or (path / "synthetic.json").exists():
+        seed = 0
+        if (path / "synthetic.json").exists():
+            seed = json.loads((path / "synthetic.json").read_text()).get("seed", 0)
+        params, head = X.init_params(seed=seed), X.DEFAULT_HEAD
+        origin = f"synthetic(seed={seed})"
+    else:
+        raise FileNotFoundError(f"no servable artifact in {path}")
+    if "serving_default" not in sigs:
+        sigs["serving_default"] = SignatureInfo("serving_default", "input_8", P.DT_FLOAT, head.out)
+    out_key = sigs["serving_default"].output_key
+    sigs.setdefault(NATIVE_SIGNATURE, SignatureInfo(NATIVE_SIGNATURE, NATIVE_INPUT_KEY, P.DT_UINT8, out_key))
+    return ModelSource(params=params, head=head, signatures=sigs, origin=origin)
+
+
+# ---------------------------------------------------------------------- executors
+class _Executor(threading.Thread):
+    """Pulls batches from a DynamicBatcher and runs them on one device."""
+
+    def __init__(self, runner: "SignatureRunner", name: str):
+        super().__init__(name=name, daemon=True)
+        self.runner = runner
+        self.stop = threading.Event()
+        self.ready = threading.Event()
+        self.error: BaseException | None = None
+
+    def run(self):
+        try:
+            self.setup()
+        except BaseException as e:  # noqa: BLE001
+            self.error = e
+            log.exception("executor %s failed to start", self.name)
+            self.ready.set()
+            return
+        self.ready.set()
+        b = self.runner.batcher
+        rt = _lib.rt()
+        while not self.stop.is_set():
+            batch = b.next_batch(self.staging_ptr(), 100_000)
+            if batch is None:
+                continue
+            t0 = time.perf_counter()
+            try:
+                out_ptr = self.execute(batch.bucket, batch.n_real)
+                b.finish(batch, out_ptr, rt.ST_OK)
+            except BaseException:  # noqa: BLE001 - fail the batch, keep serving
+                log.exception("batch %d failed on %s", batch.id, self.name)
+                b.finish(batch, 0, rt.ST_ERROR)
+                METRICS.inc("kdl_batch_errors_total", executor=self.name)
+                continue
+            dt = (time.perf_counter() - t0) * 1e3
+            METRICS.observe("kdl_batch_exec_ms", dt, executor=self.name)
+            METRICS.observe("kdl_batch_size", batch.n_real, buckets=BATCH_BUCKETS, signature=self.runner.sig.name)
+            METRICS.inc("kdl_batches_total", signature=self.runner.sig.name)
+            METRICS.inc("kdl_padded_items_total", batch.bucket - batch.n_real, signature=self.runner.sig.name)
+
+
+class GPUExecutor(_Executor):
+    def __init__(self, runner, device: int, engine_kwargs: dict):
+        super().__init__(runner, f"gpu{device}/{runner.sig.name}")
+        self.device = device
+        self.engine_kwargs = engine_kwargs
+
+    def setup(self):
+        from ..engine.tuning import tuning_path
+        from ..engine.xception import XceptionEngine
+        torch.cuda.set_device(self.device)
+        r = self.runner
+        bs = r.buckets
+        in_kind = "u8" if r.sig.input_dtype == P.DT_UINT8 else "f32"
+        self.engine = XceptionEngine(r.source.params, max_batch=bs[-1], device=f"cuda:{self.device}",
+                                     in_kind=in_kind, head=r.source.head, buckets=bs)
+        tp = tuning_path("xception", bs[-1])
+        if tp.exists():
+            self.engine.load_tuning(tp)
+        dt = torch.uint8 if in_kind == "u8" else torch.float32
+        self.staging = torch.zeros((bs[-1], IMG, IMG, 3), dtype=dt).pin_memory()
+        self.out = torch.zeros((bs[-1], self.engine.head.classes), dtype=torch.float32).pin_memory()
+        for bk in bs:                         # warm-up + capture one hipGraph per bucket
+            self.engine.program(bk, capture=True)
+            self.engine.launch(bk)
+        torch.cuda.synchronize(self.device)
+
+    def staging_ptr(self) -> int:
+        return self.staging.data_ptr()
+
+    def execute(self, bucket: int, n_real: int) -> int:
+        e = self.engine
+        with torch.cuda.stream(e.stream):
+            e.inp[:bucket].copy_(self.staging[:bucket], non_blocking=True)
+            e.launch(bucket, e.stream)
+            self.out[:bucket].copy_(e.logits[:bucket], non_blocking=True)
+        e.stream.synchronize()
+        return self.out.data_ptr()
+
+
+class CPUExecutor(_Executor):
+    def __init__(self, runner):
+        super().__init__(runner, f"cpu/{runner.sig.name}")
+
+    def setup(self):
+        bs = self.runner.buckets[-1]
+        u8 = self.runner.sig.input_dtype == P.DT_UINT8
+        self.staging = torch.zeros((bs, IMG, IMG, 3), dtype=torch.uint8 if u8 else torch.float32)
+        self.out = torch.zeros((bs, self.runner.source.head.classes), dtype=torch.float32)
+        self.u8 = u8
+
+    def staging_ptr(self) -> int:
+        return self.staging.data_ptr()
+
+    def execute(self, bucket: int, n_real: int) -> int:
+        x = self.staging[:n_real]
+        x = x.float() / 127.5 - 1.0 if self.u8 else x
+        self.out[:n_real] = X.xception_forward(self.runner.source.params, x, head=self.runner.source.head)
+        return self.out.data_ptr()
+
+
+class SignatureRunner:
+    """One C++ batcher + the executors serving one signature of one version."""
+
+    def __init__(self, sig: SignatureInfo, source: ModelSource, cfg: ServerConfig, devices: list[int]):
+        self.sig, self.source, self.cfg = sig, source, cfg
+        bp = cfg.batching
+        self.buckets = sorted(set(bp.allowed_batch_sizes)) if cfg.enable_batching else [bp.max_batch_size]
+        self.max_batch = self.buckets[-1]
+        item_bytes = IMG * IMG * 3 * (1 if sig.input_dtype == P.DT_UINT8 else 4)
+        timeout = bp.batch_timeout_micros if cfg.enable_batching else 0
+        self.batcher = _lib.rt().DynamicBatcher(max_batch_size=self.max_batch, batch_timeout_us=timeout,
+                                                max_enqueued_batches=bp.max_enqueued_batches,
+                                                allowed_batch_sizes=self.buckets, item_bytes=item_bytes,
+                                                out_cols=source.head.classes)
+        self.executors: list[_Executor] = []
+        if devices:
+            for d in devices:
+                for _ in range(max(1, cfg.executors_per_gpu)):
+                    self.executors.append(GPUExecutor(self, d, {}))
+        else:
+            self.executors.append(CPUExecutor(self))
+        for ex in self.executors:
+            ex.start()
+        for ex in self.executors:
+            ex.ready.wait()
+            if ex.error is not None:
+                raise ex.error
+        METRICS.gauge("kdl_batch_queue_items", lambda: self.batcher.stats()["queue_items"], signature=sig.name)
+
+    def predict(self, payload, n: int, deadline_us: int) -> np.ndarray:
+        """payload: buffer of n items (uint8 or f32 images); returns f32 [n, classes]."""
+        rt = _lib.rt()
+        ncls = self.source.head.classes
+        out = np.empty((n, ncls), dtype=np.float32)
+        item_bytes = IMG * IMG * 3 * (1 if self.sig.input_dtype == P.DT_UINT8 else 4)
+        mv = memoryview(payload).cast("B")
+        tickets = []
+        for s in range(0, n, self.max_batch):
+            k = min(self.max_batch, n - s)
+            chunk = mv[s * item_bytes:(s + k) * item_bytes]
+            t = self.batcher.submit(chunk, k, deadline_us)
+            if t < 0:
+                for _, tt, _ in tickets:   # drain what was already queued
+                    self.batcher.wait(tt, np.empty((1, ncls), np.float32))
+                raise ServingError("RESOURCE_EXHAUSTED" if -t == rt.ST_QUEUE_FULL else "UNAVAILABLE",
+                                   f"batcher rejected request (status {-t})")
+            tickets.append((s, t, chunk))
+        status = rt.ST_OK
+        for s, t, chunk in tickets:
+            buf = np.empty((min(self.max_batch, n - s), ncls), dtype=np.float32)
+            st = self.batcher.wait(t, buf)
+            del chunk
+            if st == rt.ST_OK:
+                out[s:s + buf.shape[0]] = buf
+            elif status == rt.ST_OK:
+                status = st
+        if status == rt.ST_DEADLINE:
+            raise ServingError("DEADLINE_EXCEEDED", "deadline exceeded while queued for batching")
+        if status != rt.ST_OK:
+            raise ServingError("INTERNAL" if status == rt.ST_ERROR else "UNAVAILABLE", f"batch failed (status {status})")
+        return out
+
+    def close(self):
+        for ex in self.executors:
+            ex.stop.set()
+        self.batcher.shutdown()
+        for ex in self.executors:
+            ex.join(timeout=5)
+
+
+class Servable:
+    """One loaded model version (all its signatures)."""
+
+    def __init__(self, name: str, version: int, source: ModelSource, cfg: ServerConfig, devices: list[int]):
+        self.name, self.version, self.source = name, version, source
+        self.signatures = source.signatures
+        self.runners: dict[str, SignatureRunner] = {}
+        self._devices, self._cfg = devices, cfg
+        self._lock = threading.Lock()
+        # serving_default is warmed eagerly (readiness = its graphs are captured)
+        self.runner("serving_default")
+
+    def runner(self, sig_name: str) -> SignatureRunner:
+        with self._lock:
+            r = self.runners.get(sig_name)
+            if r is None:
+                if sig_name not in self.signatures:
+                    raise ServingError("INVALID_ARGUMENT", f"Serving signature name: \"{sig_name}\" not found "
+                                       "in signature def")
+                r = self.runners[sig_name] = SignatureRunner(self.signatures[sig_name], self.source,
+                                                             self._cfg, self._devices)
+            return r
+
+    def close(self):
+        for r in self.runners.values():
+            r.close()
+
+
+def pick_devices(cfg: ServerConfig) -> list[int]:
+    if cfg.device == "cpu":
+        return []
+    if torch.cuda.is_available() and _lib.available():
+        n = torch.cuda.device_count()
+        k = n if cfg.gpus <= 0 else min(cfg.gpus, n)
+        return list(range(k))
+    if cfg.device == "gpu":
+        raise RuntimeError("--device gpu requested but no GPU / kdl._C available")
+    return []

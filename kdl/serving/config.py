@@ -1,0 +1,114 @@
+"""Model-server configuration: TF-Serving-compatible flags and env.
+
+The reference runs ``tensorflow/serving:2.3.0`` whose entrypoint is
+``tensorflow_model_server --port=8500 --rest_api_port=8501
+--model_name=$MODEL_NAME --model_base_path=$MODEL_BASE_PATH/$MODEL_NAME``
+(`tf-serving.dockerfile:2-5`). The same flags and env vars are
+honoured here, plus MI355X-native knobs (devices, batching buckets, executors).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import re
+from dataclasses import dataclass, field
+
+
+@dataclass
+class BatchingParams:
+    """TF-Serving BatchingParameters (text proto) subset."""
+    max_batch_size: int = 32
+    batch_timeout_micros: int = 2000
+    max_enqueued_batches: int = 1000
+    num_batch_threads: int = 1
+    allowed_batch_sizes: list[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 32])
+
+    @classmethod
+    def parse(cls, text: str) -> "BatchingParams":
+        """Parse the text-proto file format, e.g. ``max_batch_size { value: 32 }``."""
+        p = cls()
+        for key in ("max_batch_size", "batch_timeout_micros", "max_enqueued_batches", "num_batch_threads"):
+            m = re.search(rf"{key}\s*\{{\s*value\s*:\s*(\d+)\s*\}}", text)
+            if m:
+                setattr(p, key, int(m.group(1)))
+        sizes = [int(v) for v in re.findall(r"allowed_batch_sizes\s*:\s*(\d+)", text)]
+        if sizes:
+            p.allowed_batch_sizes = sizes
+        else:
+            p.allowed_batch_sizes = [b for b in p.allowed_batch_sizes if b <= p.max_batch_size]
+        if p.allowed_batch_sizes and p.allowed_batch_sizes[-1] != p.max_batch_size:
+            p.allowed_batch_sizes.append(p.max_batch_size)
+        return p
+
+
+@dataclass
+class ServerConfig:
+    port: int = 8500
+    rest_api_port: int = 8501
+    model_name: str = "clothing-model"
+    model_base_path: str = "/models/clothing-model"
+    enable_batching: bool = True
+    batching: BatchingParams = field(default_factory=BatchingParams)
+    file_system_poll_wait_seconds: int = 1
+    grpc_max_threads: int = 64
+    rest_api_num_threads: int = 16
+    device: str = "auto"          # auto | cpu | gpu
+    gpus: int = 0                 # 0 = all visible
+    executors_per_gpu: int = 1
+    synthetic: bool = False       # random-init weights when the repo has no artifact
+    labels: list[str] = field(default_factory=list)
+    host: str = "0.0.0.0"
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="kdl-model-server",
+                                 description="MI355X-native TF-Serving-compatible model server")
+    ap.add_argument("--port", type=int, default=8500)
+    ap.add_argument("--rest_api_port", type=int, default=8501)
+    ap.add_argument("--model_name", default=None)
+    ap.add_argument("--model_base_path", default=None)
+    ap.add_argument("--enable_batching", default="true")
+    ap.add_argument("--batching_parameters_file", default=None)
+    ap.add_argument("--file_system_poll_wait_seconds", type=int, default=1)
+    ap.add_argument("--grpc_max_threads", type=int, default=64)
+    ap.add_argument("--rest_api_num_threads", type=int, default=16)
+    ap.add_argument("--device", choices=["auto", "cpu", "gpu"], default="auto")
+    ap.add_argument("--gpus", type=int, default=0)
+    ap.add_argument("--executors_per_gpu", type=int, default=1)
+    ap.add_argument("--max_batch_size", type=int, default=None)
+    ap.add_argument("--batch_timeout_micros", type=int, default=None)
+    ap.add_argument("--allowed_batch_sizes", default=None, help="comma separated, e.g. 1,4,8,16,32")
+    ap.add_argument("--synthetic_model", action="store_true")
+    ap.add_argument("--host", default="0.0.0.0")
+    return ap
+
+
+def _truthy(v) -> bool:
+    return str(v).lower() in ("1", "true", "yes", "on")
+
+
+def config_from_args(argv=None, env=None) -> ServerConfig:
+    env = os.environ if env is None else env
+    a = build_parser().parse_args(argv)
+    name = a.model_name or env.get("MODEL_NAME", "clothing-model")
+    base = a.model_base_path or os.path.join(env.get("MODEL_BASE_PATH", "/models"), name)
+    bp = BatchingParams()
+    if a.batching_parameters_file:
+        with open(a.batching_parameters_file) as f:
+            bp = BatchingParams.parse(f.read())
+    if a.max_batch_size:
+        bp.max_batch_size = a.max_batch_size
+        bp.allowed_batch_sizes = [b for b in bp.allowed_batch_sizes if b < a.max_batch_size] + [a.max_batch_size]
+    if a.batch_timeout_micros is not None:
+        bp.batch_timeout_micros = a.batch_timeout_micros
+    if a.allowed_batch_sizes:
+        bp.allowed_batch_sizes = sorted(int(x) for x in a.allowed_batch_sizes.split(","))
+        bp.max_batch_size = bp.allowed_batch_sizes[-1]
+    labels = [s for s in env.get("LABELS", "").split(",") if s]
+    return ServerConfig(port=a.port, rest_api_port=a.rest_api_port, model_name=name, model_base_path=base,
+                        enable_batching=_truthy(a.enable_batching), batching=bp,
+                        file_system_poll_wait_seconds=a.file_system_poll_wait_seconds,
+                        grpc_max_threads=a.grpc_max_threads, rest_api_num_threads=a.rest_api_num_threads,
+                        device=a.device, gpus=a.gpus, executors_per_gpu=a.executors_per_gpu,
+                        synthetic=a.synthetic_model or _truthy(env.get("KDL_SYNTHETIC_MODEL", "0")),
+                        labels=labels, host=a.host)

@@ -1,0 +1,93 @@
+"""Prometheus-text metrics for the model server (SURVEY.md §5 observability).
+
+TF-Serving exposes ``/monitoring/prometheus/metrics`` on its REST port when
+monitoring is configured; the same path is served here with request counts,
+latency and batch-size histograms, queue depth and per-stage executor timings.
+The reference itself has no metrics (`model_server.py:1-70`).
+"""
+from __future__ import annotations
+
+import bisect
+import threading
+from collections import defaultdict
+
+LAT_BUCKETS_MS = [0.5, 1, 2, 3, 5, 7.5, 10, 15, 20, 30, 50, 75, 100, 200, 500, 1000, 2000, 5000, 20000]
+BATCH_BUCKETS = [1, 2, 4, 8, 16, 32, 64, 128, 256]
+
+
+class Histogram:
+    def __init__(self, buckets):
+        self.buckets = list(buckets)
+        self.counts = [0] * (len(self.buckets) + 1)
+        self.sum = 0.0
+        self.n = 0
+        self.samples: list[float] = []
+
+    def observe(self, v: float) -> None:
+        self.counts[bisect.bisect_left(self.buckets, v)] += 1
+        self.sum += v
+        self.n += 1
+        if len(self.samples) < 100_000:
+            self.samples.append(v)
+
+    def quantile(self, q: float) -> float:
+        if not self.samples:
+            return 0.0
+        s = sorted(self.samples)
+        return s[min(len(s) - 1, int(q * len(s)))]
+
+
+class Metrics:
+    def __init__(self):
+        self._lock = threading.Lock()
+        self.counters: dict[tuple, float] = defaultdict(float)
+        self.hists: dict[tuple, Histogram] = {}
+        self.gauges: dict[tuple, callable] = {}
+
+    def inc(self, name: str, value: float = 1.0, **labels) -> None:
+        with self._lock:
+            self.counters[(name, tuple(sorted(labels.items())))] += value
+
+    def observe(self, name: str, value: float, buckets=LAT_BUCKETS_MS, **labels) -> None:
+        key = (name, tuple(sorted(labels.items())))
+        with self._lock:
+            h = self.hists.get(key)
+            if h is None:
+                h = self.hists[key] = Histogram(buckets)
+            h.observe(value)
+
+    def gauge(self, name: str, fn, **labels) -> None:
+        self.gauges[(name, tuple(sorted(labels.items())))] = fn
+
+    def hist(self, name: str, **labels) -> Histogram | None:
+        return self.hists.get((name, tuple(sorted(labels.items()))))
+
+    @staticmethod
+    def _lbl(labels, extra=()) -> str:
+        items = list(labels) + list(extra)
+        if not items:
+            return ""
+        return "{" + ",".join(f'{k}="{v}"' for k, v in items) + "}"
+
+    def render(self) -> str:
+        out = []
+        with self._lock:
+            for (name, labels), v in sorted(self.counters.items()):
+                out.append(f"{name}{self._lbl(labels)} {v:g}")
+            for (name, labels), h in sorted(self.hists.items()):
+                acc = 0
+                for b, c in zip(h.buckets + ["+Inf"], h.counts):
+                    acc += c
+                    out.append(f"{name}_bucket{self._lbl(labels, [('le', b)])} {acc}")
+                out.append(f"{name}_sum{self._lbl(labels)} {h.sum:g}")
+                out.append(f"{name}_count{self._lbl(labels)} {h.n}")
+            gauges = list(self.gauges.items())
+        for (name, labels), fn in sorted(gauges, key=lambda kv: kv[0]):
+            try:
+                out.append(f"{name}{self._lbl(labels)} {float(fn()):g}")
+            except Exception:  # noqa: BLE001 - a broken gauge must not break scraping
+                pass
+        return "\n".join(out) + "\n"
+
+
+METRICS = Metrics()

@@ -1,0 +1,126 @@
+"""TF-Serving REST API (:8501) + Prometheus metrics + k8s probes.
+
+Routes (TF-Serving REST semantics):
+  GET  /v1/models/<name>[/versions/<v>]            -> model_version_status
+  GET  /v1/models/<name>[/versions/<v>]/metadata   -> signature_def
+  POST /v1/models/<name>[/versions/<v>|/labels/<l>]:predict
+       {"signature_name"?, "instances": [...]}  -> {"predictions": [...]}
+       {"signature_name"?, "inputs": ...}       -> {"outputs": ...}
+  GET  /monitoring/prometheus/metrics, /healthz (liveness), /readyz (readiness)
+"""
+from __future__ import annotations
+
+import json
+import re
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+import numpy as np
+from google.protobuf import json_format
+
+from ..ops import _lib
+from . import protos as P
+from .backend import ServingError
+from .grpc_server import signature_def_map
+from .metrics import METRICS
+from .model_repo import STATE_NAMES, ModelManager
+
+_ROUTE = re.compile(r"^/v1/models/(?P<name>[^/:]+)(?:/versions/(?P<ver>\d+)|/labels/(?P<label>[^/:]+))?"
+                    r"(?P<tail>:predict|/metadata)?/?$")
+_HTTP = {"INVALID_ARGUMENT": 400, "NOT_FOUND": 404, "DEADLINE_EXCEEDED": 504, "UNAVAILABLE": 503,
+         "RESOURCE_EXHAUSTED": 429, "UNIMPLEMENTED": 501, "INTERNAL": 500}
+
+
+def make_handler(manager: ModelManager):
+    class H(BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *a):  # quiet
+            pass
+
+        def _send(self, code: int, body, ctype="application/json"):
+            data = body if isinstance(body, bytes) else (json.dumps(body) if not isinstance(body, str) else body).encode()
+            self.send_response(code)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
+        def _err(self, e: ServingError):
+            self._send(_HTTP.get(e.code, 500), {"error": str(e)})
+
+        def do_GET(self):  # noqa: N802
+            if self.path.startswith("/monitoring/prometheus/metrics"):
+                return self._send(200, METRICS.render(), "text/plain; version=0.0.4")
+            if self.path == "/healthz":
+                return self._send(200, {"status": "alive"})
+            if self.path == "/readyz":
+                ok = manager.ready()
+                return self._send(200 if ok else 503, {"ready": ok})
+            m = _ROUTE.match(self.path)
+            if not m or m.group("tail") == ":predict":
+                return self._send(404, {"error": "not found"})
+            try:
+                ver = int(m.group("ver")) if m.group("ver") else None
+                if m.group("tail") == "/metadata":
+                    s = manager.get(m.group("name"), ver, m.group("label"))
+                    sdm = json_format.MessageToDict(signature_def_map(s))
+                    return self._send(200, {"model_spec": {"name": s.name, "signature_name": "",
+                                                           "version": str(s.version)},
+                                            "metadata": {"signature_def": sdm}})
+                if m.group("name") != manager.name:
+                    raise ServingError("NOT_FOUND", f"Could not find any versions of model {m.group('name')}")
+                st = [{"version": str(v), "state": STATE_NAMES.get(state, "UNKNOWN"),
+                       "status": {"error_code": "OK" if not msg else "UNKNOWN", "error_message": msg}}
+                      for v, state, msg in manager.status(ver)]
+                return self._send(200, {"model_version_status": st})
+            except ServingError as e:
+                return self._err(e)
+
+        def do_POST(self):  # noqa: N802
+            m = _ROUTE.match(self.path)
+            if not m or m.group("tail") != ":predict":
+                return self._send(404, {"error": "not found"})
+            try:
+                n = int(self.headers.get("Content-Length", "0"))
+                body = json.loads(self.rfile.read(n) or b"{}")
+                ver = int(m.group("ver")) if m.group("ver") else None
+                s = manager.get(m.group("name"), ver, m.group("label"))
+                runner = s.runner(body.get("signature_name") or "serving_default")
+                sig = runner.sig
+                dt = np.uint8 if sig.input_dtype == P.DT_UINT8 else np.float32
+                if "instances" in body:
+                    inst = body["instances"]
+                    if inst and isinstance(inst[0], dict):
+                        inst = [i[sig.input_key] for i in inst]
+                    x, rows = np.asarray(inst, dtype=dt), True
+                elif "inputs" in body:
+                    inp = body["inputs"]
+                    if isinstance(inp, dict):
+                        inp = inp[sig.input_key]
+                    x, rows = np.asarray(inp, dtype=dt), False
+                else:
+                    raise ServingError("INVALID_ARGUMENT", "request must contain 'instances' or 'inputs'")
+                if x.ndim != 4 or x.shape[1:] != (299, 299, 3):
+                    raise ServingError("INVALID_ARGUMENT", f"expected images [-1,299,299,3], got {list(x.shape)}")
+                x = np.ascontiguousarray(x)
+                dl = self.headers.get("X-Deadline-Ms")
+                deadline = int(_lib.rt().now_us() + float(dl) * 1e3) if dl else 0
+                out = runner.predict(x, x.shape[0], deadline).tolist()
+                METRICS.inc("kdl_requests_total", code="OK", method="RestPredict")
+                return self._send(200, {"predictions": out} if rows else {"outputs": out})
+            except ServingError as e:
+                METRICS.inc("kdl_requests_total", code=e.code, method="RestPredict")
+                return self._err(e)
+            except (ValueError, KeyError, TypeError) as e:
+                return self._err(ServingError("INVALID_ARGUMENT", str(e)))
+
+    return H
+
+
+def start_rest_server(manager: ModelManager, host: str, port: int):
+    srv = ThreadingHTTPServer((host, port), make_handler(manager))
+    srv.daemon_threads = True
+    t = threading.Thread(target=srv.serve_forever, name="rest", daemon=True)
+    t.start()
+    return srv
