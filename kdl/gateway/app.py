@@ -20,7 +20,7 @@ import grpc
 import numpy as np
 from flask import Flask, jsonify, request
 
-from ..models.xception import LABELS as DEFAULT_LABELS
+from ..labels import LABELS as DEFAULT_LABELS
 from . import preprocess as pp
 from .client import PredictionStub, make_request, process_batch_response, process_response
 

@@ -29,8 +29,7 @@ from .layers import KERAS_BN_EPS, bn_eval, maxpool_same, pad_same_nchw
 
 INPUT_SIZE = 299
 BASE_PARAMS = 20_861_480  # Keras Xception(include_top=False)
-LABELS = ["dress", "hat", "longsleeve", "outwear", "pants",
-          "shirt", "shoes", "shorts", "skirt", "t-shirt"]  # model_server.py:21-32
+from ..labels import LABELS  # noqa: E402,F401  (model_server.py:21-32)
 
 
 @dataclass(frozen=True)
