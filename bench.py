@@ -40,6 +40,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--profile-layers", action="store_true")
+    ap.add_argument("--save-tuning", default=None, help="write the autotune result (rank 0) to this path")
     a = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -65,6 +66,8 @@ def main(argv=None) -> int:
         eng.load_tuning(tp)
     elif not a.no_tune:
         eng.autotune(B)
+    if a.save_tuning and rank == 0:
+        eng.save_tuning(a.save_tuning)
     use_graph = not a.no_graph
 
     g = torch.Generator().manual_seed(1234 + rank)
