@@ -75,6 +75,8 @@ DwArgs dw_args(const py::dict& d) {
   DwArgs a{};
   a.x = P<const uint16_t>(d, "x"); a.w = P<const float>(d, "w"); a.y = P<uint16_t>(d, "y");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.C = I(d, "C"); a.relu_in = I(d, "relu_in");
+  a.cg = d.contains("cg") ? I(d, "cg") : 0; a.rb = d.contains("rb") ? I(d, "rb") : 0;
+  a.tw = d.contains("tw") ? I(d, "tw") : 0; a.seg = d.contains("seg") ? I(d, "seg") : 0;
   return a;
 }
 

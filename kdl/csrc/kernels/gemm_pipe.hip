@@ -129,10 +129,15 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
+      // raise this wave's issue priority while it streams MFMAs (guide §5 T-setprio:
+      // the other waves' glds issue / barrier arrival no longer interleave into the
+      // MFMA run)
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
   }
   wait_vm_barrier<0>();

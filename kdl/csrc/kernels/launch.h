@@ -46,6 +46,7 @@ struct DwArgs {
   uint16_t* y;
   int B, H, W, C;         // C = padded channel stride (multiple of 8)
   int relu_in;
+  int cg, rb, tw, seg;    // tile overrides (0 = host heuristic): 8-ch chunks, rows, cols, cols/item
 };
 hipError_t dw3x3(const DwArgs& a, hipStream_t s);
 
