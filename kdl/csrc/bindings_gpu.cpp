@@ -37,8 +37,12 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
   a.K = I(d, "K"); a.cin = I(d, "cin", 32); a.NF = I(d, "NF");
   a.nstore = I(d, "nstore"); a.stride = I(d, "stride", 1);
-  a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out");
+  a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out"); a.opad = I(d, "opad");
   return a;
+}
+float F(const py::dict& d, const char* k, float def) {
+  if (!d.contains(k) || d[k].is_none()) return def;
+  return d[k].cast<float>();
 }
 StemArgs stem_args(const py::dict& d) {
   StemArgs a{};
@@ -46,6 +50,32 @@ StemArgs stem_args(const py::dict& d) {
   a.bias = P<const float>(d, "bias"); a.y = P<uint16_t>(d, "y");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W");
   a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.ldy = I(d, "ldy"); a.in_kind = I(d, "in_kind");
+  // defaults = the Xception stem (3x3 s2 'valid' -> 32, normalisation folded into the weights)
+  a.KH = I(d, "KH", 3); a.KW = I(d, "KW", 3); a.stride = I(d, "stride", 2); a.pad = I(d, "pad", 0);
+  a.cout = I(d, "cout", 32); a.relu = I(d, "relu", 1);
+  const char* sk[3] = {"scale0", "scale1", "scale2"};
+  const char* hk[3] = {"shift0", "shift1", "shift2"};
+  for (int c = 0; c < 3; ++c) { a.scale[c] = F(d, sk[c], 1.f); a.shift[c] = F(d, hk[c], 0.f); }
+  return a;
+}
+GapArgs gap_args(const py::dict& d) {
+  GapArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.y = P<float>(d, "y"); a.yb = P<uint16_t>(d, "yb");
+  a.B = I(d, "B"); a.HW = I(d, "HW"); a.ldx = I(d, "ldx"); a.F = I(d, "F");
+  return a;
+}
+FcArgs fc_args(const py::dict& d) {
+  FcArgs a{};
+  a.x = P<const float>(d, "x"); a.w = P<const float>(d, "w"); a.bias = P<const float>(d, "bias");
+  a.out = P<float>(d, "out");
+  a.B = I(d, "B"); a.F = I(d, "F"); a.N = I(d, "N"); a.relu = I(d, "relu");
+  return a;
+}
+FcMfmaArgs fcm_args(const py::dict& d) {
+  FcMfmaArgs a{};
+  a.xb = P<const uint16_t>(d, "xb"); a.wp = P<const uint16_t>(d, "wp"); a.bias = P<const float>(d, "bias");
+  a.out = P<float>(d, "out");
+  a.B = I(d, "B"); a.F = I(d, "F"); a.N = I(d, "N"); a.NF = I(d, "NF"); a.relu = I(d, "relu");
   return a;
 }
 PoolAddArgs pool_args(const py::dict& d) {
@@ -118,6 +148,21 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(head_dense(a, S(s)), "head_dense");
   });
+  m.def("gap", [](py::dict d, uintptr_t s) {
+    const auto a = gap_args(d);
+    py::gil_scoped_release nogil;
+    chk(gap(a, S(s)), "gap");
+  });
+  m.def("fc", [](py::dict d, uintptr_t s) {
+    const auto a = fc_args(d);
+    py::gil_scoped_release nogil;
+    chk(fc(a, S(s)), "fc");
+  });
+  m.def("fc_mfma", [](py::dict d, uintptr_t s) {
+    const auto a = fcm_args(d);
+    py::gil_scoped_release nogil;
+    chk(fc_mfma(a, S(s)), "fc_mfma");
+  });
   m.def("resize_nearest_u8", [](py::dict d, uintptr_t s) {
     const auto a = resize_args(d);
     py::gil_scoped_release nogil;
@@ -143,6 +188,15 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_head", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_HEAD; op.name = name; op.hd = head_args(d); p.add(op);
+      })
+      .def("add_gap", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_GAP; op.name = name; op.gp = gap_args(d); p.add(op);
+      })
+      .def("add_fc", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_FC; op.name = name; op.fc = fc_args(d); p.add(op);
+      })
+      .def("add_fc_mfma", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_FC_MFMA; op.name = name; op.fcm = fcm_args(d); p.add(op);
       })
       .def("add_resize", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_RESIZE; op.name = name; op.rs = resize_args(d); p.add(op);

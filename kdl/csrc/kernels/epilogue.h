@@ -1,0 +1,33 @@
+// Shared conv-GEMM epilogue store (conv_gemm / gemm_pipe / sepconv_fused):
+// residual add, ReLU-after-residual (ResNet), and the zero-bordered output
+// layout that lets the following 3x3 'same' conv run as a bounds-check-free
+// 'valid' implicit GEMM (the 1-pixel border is zeroed once at allocation).
+#pragma once
+#include "common.h"
+#include "launch.h"
+
+namespace kdl {
+
+__device__ __forceinline__ long out_offset(const ConvGemmArgs& a, int m) {
+  if (!a.opad) return (long)m * a.ldy;
+  const int OHW = a.OH * a.OW;
+  const int b = m / OHW, rem = m - b * OHW;
+  const int oh = rem / a.OW, ow = rem - oh * a.OW;
+  return (((long)b * (a.OH + 2) + oh + 1) * (a.OW + 2) + ow + 1) * a.ldy;
+}
+
+// v: 8 bf16 (bias + optional pre-residual ReLU already applied) for row m, cols n..n+7
+__device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u32x4 v) {
+  if (a.res) {
+    const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
+  }
+  if (a.relu_out == 2) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
+  }
+  *(u32x4*)(a.y + out_offset(a, m) + n) = v;
+}
+
+}  // namespace kdl

@@ -17,6 +17,7 @@
 //   * XCD-aware bijective block remap (T1).
 #include "common.h"
 #include "launch.h"
+#include "epilogue.h"
 
 namespace kdl {
 
@@ -65,11 +66,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       m = m < a.M ? m : a.M - 1;
       const int b = m / OHW, rem = m - b * OHW;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
-      long pix;
-      if constexpr (MODE == 0)
-        pix = ((long)b * a.H + (long)oh * a.stride) * a.W + (long)ow * a.stride;
-      else
-        pix = ((long)b * a.H + oh) * a.W + ow;
+      const long pix = ((long)b * a.H + (long)oh * a.stride) * a.W + (long)ow * a.stride;
       src[i] = pix * a.ldx + 8 * (lane >> 4);
     } else {
       const int nf = n0 / 16 + (f - AF);
@@ -153,7 +150,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       const int ml = wm * FM * 16 + i * 16 + col;
       float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y;
       float v2 = acc[i][j][2] + bv.z, v3 = acc[i][j][3] + bv.w;
-      if (a.relu_out) {
+      if (a.relu_out == 1) {
         v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       }
       *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
@@ -165,14 +162,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
     if (m < a.M && n < a.nstore) {
-      u32x4 v = *(const u32x4*)(smem + r * CS + cc * 16);
-      if (a.res) {
-        const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-          v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
-      }
-      *(u32x4*)(a.y + (long)m * a.ldy + n) = v;
+      epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
     }
   }
 }

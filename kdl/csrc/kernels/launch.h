@@ -12,8 +12,8 @@ struct ConvGemmArgs {
   const uint16_t* wp;    // packed weights [NF][K/32][64][8] bf16 (BN scale folded)
   const float* bias;     // [NF*16] fp32 (BN shift)
   const float* dww;      // MODE_DW: depthwise weights [9][K] fp32
-  const uint16_t* res;   // optional residual [M][ldr] bf16 (added after ReLU)
-  uint16_t* y;           // output [M][ldy] bf16
+  const uint16_t* res;   // optional residual [M][ldr] bf16
+  uint16_t* y;           // output [M][ldy] bf16 (or a zero-bordered [B][OH+2][OW+2][ldy] if opad)
   int B, H, W;           // input spatial dims
   int OH, OW;            // output spatial dims
   int M;                 // B*OH*OW
@@ -22,8 +22,11 @@ struct ConvGemmArgs {
   int cin;               // MODE_CONV: padded input channels (multiple of 32)
   int NF;                // 16-wide output-channel fragments in the packed weights
   int nstore;            // output channels written (<= ldy)
-  int stride;            // MODE_PW spatial stride
-  int relu_in, relu_out;
+  int stride;            // spatial stride (MODE_PW / MODE_CONV)
+  int relu_in;
+  int relu_out;          // 0 none; 1 ReLU before the residual add (Xception); 2 after it (ResNet)
+  int opad;              // 1: write into the interior of a 1-pixel zero-bordered output buffer, so the
+                         //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
@@ -55,11 +58,15 @@ hipError_t dw3x3(const DwArgs& a, hipStream_t s);
 //          1 = fp32 HWC already preprocessed (TF-Serving compat input).
 struct StemArgs {
   const void* x;
-  const uint16_t* wp;     // packed [2][1][64][8]
-  const float* bias;      // [32]
+  const uint16_t* wp;     // packed [cout/16][K32][64][8], k = (ky*KW+kx)*3 + c
+  const float* bias;      // [cout]
   uint16_t* y;            // [B*OH*OW][ldy]
   int B, H, W, OH, OW, ldy;
   int in_kind;
+  int KH, KW, stride, pad, cout;  // generic KxK stride/pad conv from 3 channels (cout = 32 or 64)
+  float scale[3], shift[3];       // per-channel input normalisation applied on load (zero padding
+                                  // stays exact: padded taps are 0 in the normalised space)
+  int relu;
 };
 hipError_t stem_conv(const StemArgs& a, hipStream_t s);
 
@@ -72,6 +79,36 @@ struct PoolAddArgs {
   int pad_top, pad_left;
 };
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s);
+
+// Global average pool: x [B][HW][ldx] bf16 -> y [B][F] fp32.
+struct GapArgs {
+  const uint16_t* x;
+  float* y;               // [B][F] fp32 (may be null)
+  uint16_t* yb;           // [B][F] bf16 copy for the MFMA classifier (may be null)
+  int B, HW, ldx, F;      // F multiple of 8
+};
+hipError_t gap(const GapArgs& a, hipStream_t s);
+
+// Dense layer on pooled features: out[b][n] = sum_k x[b][k] w[k][n] + bias[n] (+ReLU), fp32.
+struct FcArgs {
+  const float* x;         // [B][F]
+  const float* w;         // [F][N] (Keras Dense / transposed torch Linear layout)
+  const float* bias;      // [N]
+  float* out;             // [B][N]
+  int B, F, N, relu;
+};
+hipError_t fc(const FcArgs& a, hipStream_t s);
+
+// MFMA classifier: out[b][n] = sum_k xb[b][k] W[n][k] + bias[n] (+ReLU), fp32 out.
+// xb: bf16 [rows >= round_up(B,16)][F] (rows >= B zero), wp: packed [NF][F/32][64][8].
+struct FcMfmaArgs {
+  const uint16_t* xb;
+  const uint16_t* wp;
+  const float* bias;
+  float* out;
+  int B, F, N, NF, relu;
+};
+hipError_t fc_mfma(const FcMfmaArgs& a, hipStream_t s);
 
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {

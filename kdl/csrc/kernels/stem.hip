@@ -1,76 +1,121 @@
-// Xception stem: block1_conv1 (3x3, stride 2, 'valid', 3 -> 32) + BN + ReLU
-// (with K1's normalisation fused).
+// Network stems: a KxK / stride / pad conv from 3 input channels + BN + ReLU,
+// with the input normalisation fused (SURVEY.md §2.5 K1+K2, §2.6 ResNet 7x7 stem).
 //
-// K = 27 (padded to one 32-deep MFMA step). Each lane gathers its own A fragment
-// straight from the image (8 scalars: tap*3 + channel), so there is no LDS at all;
-// the whole op is one MFMA per 16x16 output tile. For uint8 input the Xception
-// preprocessing x/127.5 - 1 is folded into the weights on the host (exact: the
-// conv is 'valid', every tap is in-bounds), so raw pixels are consumed directly
-// and the f32 normalised image never exists.
+//   Xception block1_conv1: 3x3 s2 'valid', 3 -> 32 (K = 27 -> one 32-deep step);
+//       for uint8 input x/127.5-1 is folded into the weights (exact: 'valid').
+//   ResNet-50 conv1:       7x7 s2 pad 3, 3 -> 64 (K = 147 -> 5 steps); the
+//       torchvision mean/std normalisation is applied on load (scale/shift per
+//       channel) so zero padding stays exact.
+//
+// Each lane gathers its own A fragment straight from the image (8 scalars:
+// k = (ky*KW + kx)*3 + c), so there is no LDS at all. The (ky, kx, c) of a lane's
+// 8 k-slots depend only on the k-step, not on the pixel, and are computed once
+// per step for both 16-row fragments of the wave.
 #include "common.h"
 #include "launch.h"
 
 namespace kdl {
 
-template <int IN_KIND>
+template <int IN_KIND, int NF>
 __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int M = a.B * a.OH * a.OW;
   const int OHW = a.OH * a.OW;
   const int m_wave = blockIdx.x * 128 + wave * 32;
+  const int KK = a.KH * a.KW * 3;
+  const int KT = (KK + 31) >> 5;
 
-  s16x8 bw[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) bw[j] = *(const s16x8*)(a.wp + (j * 64 + lane) * 8);
-
-  const int kq = 8 * (lane >> 4);
+  long pbase[2];
+  int ih0[2], iw0[2];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     int m = m_wave + f * 16 + (lane & 15);
-    const bool mvalid = m < M;
-    m = mvalid ? m : M - 1;
+    m = m < M ? m : M - 1;
     const int b = m / OHW, rem = m - b * OHW;
     const int oh = rem / a.OW, ow = rem - oh * a.OW;
-    const long base = ((long)b * a.H + 2 * oh) * a.W + 2 * ow;  // pixel index of tap (0,0)
-    s16x8 af;
+    ih0[f] = oh * a.stride - a.pad;
+    iw0[f] = ow * a.stride - a.pad;
+    pbase[f] = (long)b * a.H * a.W;
+  }
+  f32x4 acc[2][NF];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int kq = 8 * (lane >> 4);
+  for (int ks = 0; ks < KT; ++ks) {
+    int dy[8], dx[8], ch[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = kq + j;
-      float v = 0.f;
-      if (k < 27) {
-        const int tap = k / 3, c = k - 3 * (k / 3);
-        const long p = base + (long)(tap / 3) * a.W + (tap % 3);
-        if constexpr (IN_KIND == 0) v = (float)((const uint8_t*)a.x)[p * 3 + c];
-        else v = ((const float*)a.x)[p * 3 + c];
-      }
-      af[j] = (short)f2bf(v);
+      const int k = ks * 32 + kq + j;
+      const int tap = k / 3;
+      ch[j] = k < KK ? k - 3 * tap : -1;
+      dy[j] = tap / a.KW;
+      dx[j] = tap - dy[j] * a.KW;
     }
-    f32x4 acc[2];
+    s16x8 bw[NF];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[j] = mfma16(bw[j], af, (f32x4){0.f, 0.f, 0.f, 0.f});
-    // lane holds Y[m_tile + (lane&15)][16j + 4*(lane>>4) + r]
+    for (int j = 0; j < NF; ++j) bw[j] = *(const s16x8*)(a.wp + (((long)j * KT + ks) * 64 + lane) * 8);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      s16x8 af;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ih = ih0[f] + dy[j], iw = iw0[f] + dx[j];
+        float v = 0.f;
+        if (ch[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
+          const long p = (pbase[f] + (long)ih * a.W + iw) * 3 + ch[j];
+          float raw;
+          if constexpr (IN_KIND == 0) raw = (float)((const uint8_t*)a.x)[p];
+          else raw = ((const float*)a.x)[p];
+          const int c = ch[j];
+          v = raw * (c == 0 ? a.scale[0] : c == 1 ? a.scale[1] : a.scale[2]) +
+              (c == 0 ? a.shift[0] : c == 1 ? a.shift[1] : a.shift[2]);
+        }
+        af[j] = (short)f2bf(v);
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[f][j] = mfma16(bw[j], af, acc[f][j]);
+    }
+  }
+  // lane holds Y[m_tile + (lane&15)][16j + 4*(lane>>4) + r]
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
     const int mo = m_wave + f * 16 + (lane & 15);
     if (mo < M) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NF; ++j) {
         const int n = 16 * j + 4 * (lane >> 4);
         const float4 bv = *(const float4*)(a.bias + n);
-        const float v0 = fmaxf(acc[j][0] + bv.x, 0.f), v1 = fmaxf(acc[j][1] + bv.y, 0.f);
-        const float v2 = fmaxf(acc[j][2] + bv.z, 0.f), v3 = fmaxf(acc[j][3] + bv.w, 0.f);
+        float v0 = acc[f][j][0] + bv.x, v1 = acc[f][j][1] + bv.y;
+        float v2 = acc[f][j][2] + bv.z, v3 = acc[f][j][3] + bv.w;
+        if (a.relu) {
+          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        }
         *(u32x2*)(a.y + (long)mo * a.ldy + n) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
       }
     }
   }
 }
 
+template <int IN_KIND>
+static hipError_t launch_stem(const StemArgs& a, dim3 grid, hipStream_t s) {
+  switch (a.cout) {
+    case 32: hipLaunchKernelGGL((stem_kernel<IN_KIND, 2>), grid, dim3(256), 0, s, a); break;
+    case 64: hipLaunchKernelGGL((stem_kernel<IN_KIND, 4>), grid, dim3(256), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t stem_conv(const StemArgs& a, hipStream_t s) {
   const int M = a.B * a.OH * a.OW;
-  if (M <= 0 || a.ldy < 32) return hipErrorInvalidValue;
+  if (M <= 0 || a.ldy < a.cout || a.KH <= 0 || a.KW <= 0 || a.stride <= 0) return hipErrorInvalidValue;
   const dim3 grid((M + 127) / 128);
-  if (a.in_kind == 0) hipLaunchKernelGGL(stem_kernel<0>, grid, dim3(256), 0, s, a);
-  else if (a.in_kind == 1) hipLaunchKernelGGL(stem_kernel<1>, grid, dim3(256), 0, s, a);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
+  if (a.in_kind == 0) return launch_stem<0>(a, grid, s);
+  if (a.in_kind == 1) return launch_stem<1>(a, grid, s);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace kdl

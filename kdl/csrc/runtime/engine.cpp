@@ -17,6 +17,9 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_RESIZE: return resize_nearest_u8(op.rs, s);
     case OP_MEMSET: return hipMemsetAsync(op.mem_ptr, 0, op.mem_bytes, s);
     case OP_DW: return dw3x3(op.dw, s);
+    case OP_GAP: return gap(op.gp, s);
+    case OP_FC: return fc(op.fc, s);
+    case OP_FC_MFMA: return fc_mfma(op.fcm, s);
   }
   return hipErrorInvalidValue;
 }

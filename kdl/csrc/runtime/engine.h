@@ -15,7 +15,7 @@
 
 namespace kdl {
 
-enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6 };
+enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6, OP_GAP = 7, OP_FC = 8, OP_FC_MFMA = 9 };
 
 struct Op {
   OpKind kind;
@@ -27,6 +27,9 @@ struct Op {
   HeadArgs hd{};
   ResizeArgs rs{};
   DwArgs dw{};
+  GapArgs gp{};
+  FcArgs fc{};
+  FcMfmaArgs fcm{};
   void* mem_ptr = nullptr;
   size_t mem_bytes = 0;
 };

@@ -1,0 +1,180 @@
+"""Model-agnostic MI355X executor machinery shared by every model family.
+
+A model engine lowers its network into a list of ``Step`` s (fused HIP launches
+over statically planned NHWC bf16 buffers). This base class owns what does not
+depend on the network: one native ``Program`` per (batch bucket, capture) with
+a hipGraph per bucket, per-op profiling, per-layer tile autotuning over the
+conv-GEMM config table, and the tuning-table round trip
+(``kdl/tuning/<model>_b<batch>.json``). The reference equivalent is a
+TF-Serving servable's session run (`tf-serving.dockerfile:2-5`).
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import torch
+
+from ..ops import _lib
+from ..ops.conv import MODE_DW, ConvGemmLayer
+
+
+@dataclass
+class Step:
+    kind: str                  # conv | stem | pool | head | gap | fc | ...
+    name: str
+    layer: object = None
+    src: str = ""
+    dst: str = ""
+    res: str | None = None
+    geom: tuple = ()           # (H, W, OH, OW) per image
+    extra: dict = field(default_factory=dict)
+
+
+class EngineBase:
+    model_name = "model"
+
+    def __init__(self, device, max_batch: int, buckets=None):
+        self.device = torch.device(device)
+        self.max_batch = max_batch
+        self.buckets = sorted(set(buckets or [max_batch]))
+        assert self.buckets[-1] <= max_batch
+        self.steps: list[Step] = []
+        self.programs: dict[tuple[int, bool, int], object] = {}
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.inputs: list[torch.Tensor] = []   # input slots (self.inp is slot 0)
+        self._slot = 0
+
+    # ---------------------------------------------------------------- input slots
+    def input_ptr(self) -> int:
+        """Device pointer of the input slot the program being built reads."""
+        return _lib.ptr(self.inputs[self._slot] if self.inputs else self.inp)
+
+    def add_input_slots(self, n: int) -> list[torch.Tensor]:
+        """Extra static input buffers, each with its own captured graphs, so a
+        pipelined caller can H2D batch i+1 into one slot while the graph of batch i
+        reads another (no device-to-device staging copy on the compute stream)."""
+        if not self.inputs:
+            self.inputs = [self.inp]
+        while len(self.inputs) < n:
+            self.inputs.append(torch.zeros_like(self.inp))
+        return self.inputs
+
+    # ---------------------------------------------------------------- hooks
+    def _emit(self, prog, step: Step, b: int) -> None:
+        raise NotImplementedError
+
+    def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
+        """Emit (prog) or launch now (prog=None) one conv step with an explicit variant."""
+        raise NotImplementedError
+
+    # ---------------------------------------------------------------- programs
+    def conv_steps(self) -> list[Step]:
+        return [s for s in self.steps if s.kind == "conv"]
+
+    def program(self, b: int, capture: bool = True, slot: int = 0):
+        key = (b, capture, slot)
+        if key in self.programs:
+            return self.programs[key]
+        assert 1 <= b <= self.max_batch
+        prog = _lib.lib().Program()
+        self._slot = slot
+        try:
+            for step in self.steps:
+                self._emit(prog, step, b)
+        finally:
+            self._slot = 0
+        if capture:
+            with torch.cuda.device(self.device):
+                prog.capture(int(self.stream.cuda_stream))
+        self.programs[key] = prog
+        return prog
+
+    def invalidate(self) -> None:
+        self.programs.clear()
+
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        raise ValueError(f"batch {n} exceeds max bucket {self.buckets[-1]}")
+
+    def launch(self, b: int, stream: torch.cuda.Stream | None = None, capture: bool = True,
+               slot: int = 0) -> None:
+        """Run the forward for the first ``b`` images already in input slot ``slot``."""
+        s = stream or self.stream
+        self.program(b, capture, slot).launch(int(s.cuda_stream))
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, capture: bool = True) -> torch.Tensor:
+        """x: [n, H, W, 3] in the engine's input dtype, any device -> fp32 logits [n, classes]."""
+        n = x.shape[0]
+        assert tuple(x.shape[1:]) == tuple(self.inp.shape[1:]), (x.shape, self.inp.shape)
+        assert x.dtype == self.inp.dtype, (x.dtype, self.inp.dtype)
+        b = self.bucket_for(n)
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.inp[:n].copy_(x, non_blocking=True)
+            self.launch(b, self.stream, capture)
+            out = self.logits[:n].clone()
+        cur.wait_stream(self.stream)
+        return out
+
+    # ---------------------------------------------------------------- observability / tuning
+    def profile(self, b: int, iters: int = 20) -> list[tuple[str, float]]:
+        prog = self.program(b, capture=False)
+        ms = prog.profile(int(self.stream.cuda_stream), iters)
+        return list(zip(prog.op_names(), ms))
+
+    def _variants(self, step: Step) -> list[tuple[bool, int]]:
+        return step.layer.variants(step.geom[1])
+
+    def autotune(self, b: int, iters: int = 10, verbose: bool = False) -> dict[str, list[int]]:
+        """Pick the fastest (split, tile config) per conv layer by timing on the device."""
+        s = self.stream
+        chosen = {}
+        with torch.cuda.stream(s):
+            for step in self.conv_steps():
+                lay: ConvGemmLayer = step.layer
+                best = None
+                for split, cfg in self._variants(step):
+                    def run():
+                        self._emit_conv(None, step, b, split=split, cfg=cfg)
+                    for _ in range(2):
+                        run()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(s)
+                    for _ in range(iters):
+                        run()
+                    e1.record(s)
+                    e1.synchronize()
+                    t = e0.elapsed_time(e1) / iters
+                    if best is None or t < best[0]:
+                        best = (t, split, cfg)
+                    if verbose:
+                        print(f"  {step.name:24s} split={int(split)} cfg {cfg}: {t * 1e3:8.1f} us", flush=True)
+                lay.split, lay.cfg = best[1], best[2]
+                chosen[step.name] = [int(best[1]), best[2]]
+        self.invalidate()
+        return chosen
+
+    def tuning(self) -> dict[str, list[int]]:
+        return {s.name: [int(s.layer.split), s.layer.cfg] for s in self.conv_steps()}
+
+    def save_tuning(self, path) -> None:
+        Path(path).write_text(json.dumps(self.tuning(), indent=1))
+
+    def load_tuning(self, path) -> None:
+        self.apply_tuning(json.loads(Path(path).read_text()))
+
+    def apply_tuning(self, d: dict) -> None:
+        for s in self.conv_steps():
+            v = d.get(s.name)
+            if v is None:
+                continue
+            split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
+            if cfg in s.layer.candidates and (not split or s.layer.mode == MODE_DW):
+                s.layer.split, s.layer.cfg = split, cfg
+        self.invalidate()

@@ -1,0 +1,54 @@
+"""Model-family registry: oracle params + MI355X engine + benchmark metadata.
+
+One entry per BASELINE.json config family the stack serves.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable
+
+
+@dataclass(frozen=True)
+class ModelInfo:
+    name: str
+    input_size: int
+    classes: int
+    params_total: int
+    description: str
+    init_params: Callable
+    engine: Callable          # (params, max_batch, device, **kw) -> EngineBase
+    oracle: Callable          # (params, uint8 NHWC) -> fp32 logits
+
+
+def _xception():
+    from ..models import xception as X
+    from .xception import XceptionEngine
+    return ModelInfo("xception", X.INPUT_SIZE, 10, 21_067_390,
+                     "Keras Xception 299x299 + clothing head (21,067,390 params)",
+                     lambda seed=0: X.init_params(seed=seed),
+                     lambda p, max_batch, device, **kw: XceptionEngine(p, max_batch=max_batch, device=device,
+                                                                       in_kind="u8", **kw),
+                     lambda p, x: X.xception_forward(p, x.float() / 127.5 - 1.0))
+
+
+def _resnet50():
+    from ..models import resnet as R
+    from .resnet import ResNetEngine
+    return ModelInfo("resnet50", R.INPUT_SIZE, 1000, R.TOTAL_PARAMS,
+                     "ResNet-50 v1.5 224x224 (torchvision layout, 25,557,032 params)",
+                     lambda seed=0: R.init_params(seed=seed),
+                     lambda p, max_batch, device, **kw: ResNetEngine(p, max_batch=max_batch, device=device, **kw),
+                     R.resnet_forward)
+
+
+_FACTORIES = {"xception": _xception, "resnet50": _resnet50}
+
+
+def models() -> list[str]:
+    return sorted(_FACTORIES)
+
+
+def get(name: str) -> ModelInfo:
+    if name not in _FACTORIES:
+        raise KeyError(f"unknown model {name!r}; known: {', '.join(models())}")
+    return _FACTORIES[name]()

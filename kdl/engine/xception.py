@@ -17,9 +17,6 @@ The reference equivalent is TF-Serving's SavedModel session run
 """
 from __future__ import annotations
 
-import json
-import time
-from dataclasses import dataclass, field
 from pathlib import Path
 
 import torch
@@ -30,37 +27,22 @@ from ..ops import _lib
 from ..ops.conv import (MODE_CONV, MODE_DW, MODE_PW, ConvGemmLayer, Geometry,
                         conv_weights_nk)
 from ..ops.pack import bn_scale_shift, pack_fragments, round_up
+from .base import EngineBase, Step
 
 
-@dataclass
-class Step:
-    kind: str                  # conv | stem | pool | head
-    name: str
-    layer: object = None
-    src: str = ""
-    dst: str = ""
-    res: str | None = None
-    geom: tuple = ()           # (H, W, OH, OW) per image
-    extra: dict = field(default_factory=dict)
+class XceptionEngine(EngineBase):
+    model_name = "xception"
 
-
-class XceptionEngine:
     def __init__(self, params: dict, max_batch: int = 32, device: str | torch.device = "cuda",
                  in_kind: str = "u8", head: X.Head = X.DEFAULT_HEAD, buckets=None,
                  tune_file: str | Path | None = None):
-        self.device = torch.device(device)
-        self.max_batch = max_batch
+        super().__init__(device, max_batch, buckets)
         self.in_kind = in_kind
         self.head = head
         self.size = X.INPUT_SIZE
-        self.buckets = sorted(set(buckets or [max_batch]))
-        assert self.buckets[-1] <= max_batch
-        self.steps: list[Step] = []
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
         self._alloc()
-        self.stream = torch.cuda.Stream(device=self.device)
-        self.programs: dict[int, object] = {}
         if tune_file and Path(tune_file).exists():
             self.load_tuning(tune_file)
 
@@ -178,12 +160,9 @@ class XceptionEngine:
         self.dwtmp = torch.zeros(n, dtype=torch.bfloat16, device=dev)
 
     # ------------------------------------------------------------------ programs
-    def conv_steps(self) -> list[Step]:
-        return [s for s in self.steps if s.kind == "conv"]
-
     def _ptr(self, name: str) -> int:
         if name == "input":
-            return _lib.ptr(self.inp)
+            return self.input_ptr()
         if name == "logits":
             return _lib.ptr(self.logits)
         return _lib.ptr(self.bufs[name])
@@ -191,15 +170,12 @@ class XceptionEngine:
     def _emit(self, prog, step: Step, b: int) -> None:
         H, W, OH, OW = step.geom
         if step.kind == "stem":
-            prog.add_stem(step.name, dict(x=self._ptr("input"), wp=_lib.ptr(self.stem_wp),
+            prog.add_stem(step.name, dict(x=self.input_ptr(), wp=_lib.ptr(self.stem_wp),
                                           bias=_lib.ptr(self.stem_bias), y=self._ptr(step.dst),
                                           B=b, H=H, W=W, OH=OH, OW=OW, ldy=32,
                                           in_kind=0 if self.in_kind == "u8" else 1))
         elif step.kind == "conv":
-            lay: ConvGemmLayer = step.layer
-            lay.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
-                     res=self._ptr(step.res) if step.res else None, ldx=self.shapes[step.src][2],
-                     ldr=self.shapes[step.res][2] if step.res else None, tmp=_lib.ptr(self.dwtmp))
+            self._emit_conv(prog, step, b)
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=self._ptr(step.res),
                                               y=self._ptr(step.dst), B=b, H=H, W=W, OH=OH, OW=OW,
@@ -213,109 +189,12 @@ class XceptionEngine:
                                           B=b, HW=H * W, ldx=self.shapes[step.src][2],
                                           F=hd.features, H1=hd.hidden_units, NC=hd.classes))
 
-    def program(self, b: int, capture: bool = True):
-        key = (b, capture)
-        if key in self.programs:
-            return self.programs[key]
-        assert 1 <= b <= self.max_batch
-        prog = _lib.lib().Program()
-        for step in self.steps:
-            self._emit(prog, step, b)
-        if capture:
-            with torch.cuda.device(self.device):
-                prog.capture(int(self.stream.cuda_stream))
-        self.programs[key] = prog
-        return prog
-
-    def invalidate(self) -> None:
-        self.programs.clear()
-
-    def bucket_for(self, n: int) -> int:
-        for b in self.buckets:
-            if b >= n:
-                return b
-        raise ValueError(f"batch {n} exceeds max bucket {self.buckets[-1]}")
-
-    # ------------------------------------------------------------------ execution
-    def launch(self, b: int, stream: torch.cuda.Stream | None = None, capture: bool = True) -> None:
-        """Run the forward for the first ``b`` images already in ``self.inp``."""
-        s = stream or self.stream
-        self.program(b, capture).launch(int(s.cuda_stream))
-
-    @torch.no_grad()
-    def forward(self, x: torch.Tensor, capture: bool = True) -> torch.Tensor:
-        """x: uint8 (or f32 for in_kind='f32') [n,299,299,3] on any device -> f32 logits [n,10]."""
-        n = x.shape[0]
-        assert tuple(x.shape[1:]) == (self.size, self.size, 3), x.shape
-        assert x.dtype == self.inp.dtype, (x.dtype, self.inp.dtype)
-        b = self.bucket_for(n)
-        cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):
-            self.inp[:n].copy_(x, non_blocking=True)
-            self.launch(b, self.stream, capture)
-            out = self.logits[:n].clone()
-        cur.wait_stream(self.stream)
-        return out
-
-    # ------------------------------------------------------------------ observability
-    def profile(self, b: int, iters: int = 20) -> list[tuple[str, float]]:
-        prog = self.program(b, capture=False)
-        ms = prog.profile(int(self.stream.cuda_stream), iters)
-        return list(zip(prog.op_names(), ms))
-
-    def autotune(self, b: int, iters: int = 10, verbose: bool = False) -> dict[str, int]:
-        """Pick the fastest tile config per conv layer by timing on the device."""
-        s = self.stream
-        chosen = {}
-        with torch.cuda.stream(s):
-            for step in self.conv_steps():
-                lay: ConvGemmLayer = step.layer
-                H, W, OH, OW = step.geom
-                g = Geometry(b, H, W, OH, OW)
-                x, y = self.bufs[step.src], self.bufs[step.dst]
-                res = self.bufs[step.res] if step.res else None
-                best = None
-                for split, cfg in lay.variants(W):
-                    def run():
-                        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res),
-                                 ldx=self.shapes[step.src][2],
-                                 ldr=self.shapes[step.res][2] if step.res else None,
-                                 tmp=_lib.ptr(self.dwtmp), split=split, cfg=cfg)
-                    for _ in range(2):
-                        run()
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record(s)
-                    for _ in range(iters):
-                        run()
-                    e1.record(s)
-                    e1.synchronize()
-                    t = e0.elapsed_time(e1) / iters
-                    if best is None or t < best[0]:
-                        best = (t, split, cfg)
-                    if verbose:
-                        print(f"  {step.name:24s} split={int(split)} cfg {cfg}: {t * 1e3:8.1f} us", flush=True)
-                lay.split, lay.cfg = best[1], best[2]
-                chosen[step.name] = [int(best[1]), best[2]]
-        self.invalidate()
-        return chosen
-
-    def tuning(self) -> dict[str, list[int]]:
-        return {s.name: [int(s.layer.split), s.layer.cfg] for s in self.conv_steps()}
-
-    def save_tuning(self, path) -> None:
-        Path(path).write_text(json.dumps(self.tuning(), indent=1))
-
-    def load_tuning(self, path) -> None:
-        d = json.loads(Path(path).read_text())
-        for s in self.conv_steps():
-            v = d.get(s.name)
-            if v is None:
-                continue
-            split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
-            if cfg in s.layer.candidates and (not split or s.layer.mode == MODE_DW):
-                s.layer.split, s.layer.cfg = split, cfg
-        self.invalidate()
+    def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
+        H, W, OH, OW = step.geom
+        step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
+                        res=self._ptr(step.res) if step.res else None, ldx=self.shapes[step.src][2],
+                        ldr=self.shapes[step.res][2] if step.res else None, tmp=_lib.ptr(self.dwtmp),
+                        split=split, cfg=cfg)
 
     def flops_per_image(self) -> float:
         return 2 * 8.356e9

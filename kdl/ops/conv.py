@@ -101,11 +101,12 @@ class ConvGemmLayer:
 
     def __init__(self, name: str, mode: int, w_nk: torch.Tensor, bias: torch.Tensor, *,
                  cin_pad: int, n: int, stride: int = 1, dww: torch.Tensor | None = None,
-                 relu_in: bool = False, relu_out: bool = False, device="cuda",
+                 relu_in: bool = False, relu_out: bool | int = False, device="cuda",
                  candidates: list[int] | None = None):
         self.name, self.mode, self.n = name, mode, n
         self.cin_pad, self.stride = cin_pad, stride
-        self.relu_in, self.relu_out = relu_in, relu_out
+        # relu_out: 0/False none, 1/True ReLU before the residual add, 2 ReLU after it
+        self.relu_in, self.relu_out = relu_in, int(relu_out)
         self.K = w_nk.shape[1]
         assert self.K % 32 == 0, (name, self.K)
         self.ldy = round_up(n, 32)
@@ -142,7 +143,7 @@ class ConvGemmLayer:
 
     def emit(self, prog, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
              ldr: int | None = None, tmp: int | None = None, split: bool | None = None,
-             cfg: int | None = None) -> None:
+             cfg: int | None = None, opad: int = 0) -> None:
         """Append this layer's launches to a native Program (or launch now if prog is None)."""
         split = self.split if split is None else split
         cfg = self.cfg if cfg is None else cfg
@@ -150,7 +151,7 @@ class ConvGemmLayer:
         if self.mode == MODE_DW and split:
             assert tmp is not None, "split separable conv needs a scratch buffer"
             da = self.dw_args(x, tmp, g, ldx)
-            ga = self.args(tmp, y, g, res, ldx=self.cin_pad, ldr=ldr, cfg=cfg)
+            ga = self.args(tmp, y, g, res, ldx=self.cin_pad, ldr=ldr, cfg=cfg, opad=opad)
             if prog is None:
                 s = _lib.stream_ptr()
                 C.dw3x3(da, s)
@@ -159,7 +160,7 @@ class ConvGemmLayer:
                 prog.add_dw(self.name + "/dw", da)
                 prog.add_conv_gemm(self.name, MODE_PW, cfg, ga)
             return
-        ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg)
+        ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
         if prog is None:
             C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
         else:
@@ -170,34 +171,37 @@ class ConvGemmLayer:
         return round_up(self.n, cfg_tile(cfg)[1]) // 16
 
     def args(self, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
-             ldr: int | None = None, cfg: int | None = None) -> dict:
+             ldr: int | None = None, cfg: int | None = None, opad: int = 0) -> dict:
         return dict(x=x, wp=_lib.ptr(self.wp), bias=_lib.ptr(self.bias),
                     dww=_lib.ptr(self.dww), res=res, y=y,
                     B=g.B, H=g.H, W=g.W, OH=g.OH, OW=g.OW, M=g.M,
                     ldx=ldx if ldx is not None else self.cin_pad, ldy=self.ldy,
                     ldr=ldr if ldr is not None else self.ldy,
                     K=self.K, cin=self.cin_pad, NF=self.nf(cfg), nstore=self.ldy,
-                    stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out))
+                    stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out),
+                    opad=int(opad))
 
     def launch(self, x: torch.Tensor, y: torch.Tensor, g: Geometry, res: torch.Tensor | None = None,
-               cfg: int | None = None, split: bool = False, tmp: torch.Tensor | None = None) -> None:
+               cfg: int | None = None, split: bool = False, tmp: torch.Tensor | None = None,
+               opad: int = 0) -> None:
         """Eager launch on torch tensors (shape-checked on the host first)."""
-        self.check(x, y, g, res)
+        self.check(x, y, g, res, opad)
         if split:
             if tmp is None:
                 tmp = torch.empty(g.M * self.cin_pad, dtype=torch.bfloat16, device=x.device)
             assert tmp.numel() >= g.M * self.cin_pad
-        self.emit(None, _lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res), tmp=_lib.ptr(tmp), split=split, cfg=cfg)
+        self.emit(None, _lib.ptr(x), _lib.ptr(y), g, _lib.ptr(res), tmp=_lib.ptr(tmp), split=split, cfg=cfg,
+                  opad=opad)
 
-    def check(self, x, y, g: Geometry, res=None) -> None:
+    def check(self, x, y, g: Geometry, res=None, opad: int = 0) -> None:
         assert x.dtype == torch.bfloat16 and y.dtype == torch.bfloat16
         assert x.is_contiguous() and y.is_contiguous()
         assert x.numel() >= g.B * g.H * g.W * self.cin_pad, (self.name, x.shape)
-        assert y.numel() >= g.M * self.ldy, (self.name, y.shape)
+        assert y.numel() >= g.B * (g.OH + 2 * opad) * (g.OW + 2 * opad) * self.ldy, (self.name, y.shape)
         if self.mode == MODE_DW:
             assert g.OH == g.H and g.OW == g.W
         elif self.mode == MODE_CONV:
-            assert g.OH == g.H - 2 and g.OW == g.W - 2
+            assert g.OH == (g.H - 3) // self.stride + 1 and g.OW == (g.W - 3) // self.stride + 1
         else:
             assert g.OH == (g.H - 1) // self.stride + 1 and g.OW == (g.W - 1) // self.stride + 1
         if res is not None:

@@ -27,9 +27,10 @@ def conv_gemm_ref(lay: ConvGemmLayer, x: torch.Tensor, g: Geometry, res: torch.T
         a = xs[:, ::lay.stride, ::lay.stride, :].reshape(g.M, lay.cin_pad)
     elif lay.mode == MODE_CONV:
         cols = []
+        st = lay.stride
         for dy in range(3):
             for dx in range(3):
-                cols.append(xs[:, dy:dy + g.OH, dx:dx + g.OW, :])
+                cols.append(xs[:, dy:dy + st * (g.OH - 1) + 1:st, dx:dx + st * (g.OW - 1) + 1:st, :])
         a = torch.cat(cols, dim=-1).reshape(g.M, 9 * lay.cin_pad)
     else:
         xin = torch.relu(xs) if lay.relu_in else xs
@@ -38,12 +39,14 @@ def conv_gemm_ref(lay: ConvGemmLayer, x: torch.Tensor, g: Geometry, res: torch.T
         a = F.conv2d(xp, dw, groups=lay.cin_pad).permute(0, 2, 3, 1).reshape(g.M, lay.cin_pad)
         a = _bf(a)
     y = a @ w.t() + lay.bias[: lay.n].to(x.device).float()
-    if lay.relu_out:
+    if lay.relu_out == 1:
         y = torch.relu(y)
     out = torch.zeros(g.M, lay.ldy, device=x.device)
     out[:, : lay.n] = y
     if res is not None:
         out = _bf(out) + res.float().view(g.M, -1)[:, : lay.ldy]
+    if lay.relu_out == 2:
+        out = torch.relu(out)
     return out
 
 

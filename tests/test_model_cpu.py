@@ -76,3 +76,14 @@ def test_closed_form_is_not_pil():
     s = 534 / 299
     assert int((149 + 0.5) * s) == 267
     assert pp.nearest_indices(534, 299)[149] == 266
+
+
+def test_resnet50_oracle_shapes_and_cost():
+    from kdl.models import resnet as R
+    assert R.count_params() == R.TOTAL_PARAMS == 25_557_032   # torchvision resnet50
+    assert abs(R.macs_per_image() / 1e9 - 4.09) < 0.01
+    p = R.init_params(seed=1, calibrate=False)
+    x = torch.randint(0, 256, (1, 224, 224, 3), dtype=torch.uint8)
+    y1, y2 = R.resnet_forward(p, x), R.resnet_forward(p, x)
+    assert y1.shape == (1, 1000) and torch.equal(y1, y2)
+    assert [b.stride for b in R.blocks()].count(2) == 3          # v1.5: stride on conv2 of 3 stages
