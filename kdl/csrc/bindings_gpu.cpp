@@ -71,6 +71,36 @@ FcArgs fc_args(const py::dict& d) {
   a.B = I(d, "B"); a.F = I(d, "F"); a.N = I(d, "N"); a.relu = I(d, "relu");
   return a;
 }
+PatchifyArgs patch_args(const py::dict& d) {
+  PatchifyArgs a{};
+  a.x = P<const uint8_t>(d, "x"); a.y = P<uint16_t>(d, "y");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.P = I(d, "P"); a.ldy = I(d, "ldy");
+  const char* sk[3] = {"scale0", "scale1", "scale2"};
+  const char* hk[3] = {"shift0", "shift1", "shift2"};
+  for (int c = 0; c < 3; ++c) { a.scale[c] = F(d, sk[c], 1.f); a.shift[c] = F(d, hk[c], 0.f); }
+  return a;
+}
+EmbedArgs embed_args(const py::dict& d) {
+  EmbedArgs a{};
+  a.x = P<uint16_t>(d, "x"); a.cls = P<const float>(d, "cls"); a.pos = P<const float>(d, "pos");
+  a.B = I(d, "B"); a.T = I(d, "T"); a.D = I(d, "D");
+  return a;
+}
+LnArgs ln_args(const py::dict& d) {
+  LnArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.y = P<uint16_t>(d, "y");
+  a.gamma = P<const float>(d, "gamma"); a.beta = P<const float>(d, "beta");
+  a.rows = d["rows"].cast<long>(); a.D = I(d, "D"); a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy");
+  a.eps = F(d, "eps", 1e-6f);
+  return a;
+}
+AttnArgs attn_args(const py::dict& d) {
+  AttnArgs a{};
+  a.qkv = P<const uint16_t>(d, "qkv"); a.out = P<uint16_t>(d, "out");
+  a.B = I(d, "B"); a.T = I(d, "T"); a.H = I(d, "H"); a.dh = I(d, "dh", 64);
+  a.scale = F(d, "scale", 0.125f);
+  return a;
+}
 FcMfmaArgs fcm_args(const py::dict& d) {
   FcMfmaArgs a{};
   a.xb = P<const uint16_t>(d, "xb"); a.wp = P<const uint16_t>(d, "wp"); a.bias = P<const float>(d, "bias");
@@ -158,6 +188,26 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(fc(a, S(s)), "fc");
   });
+  m.def("patchify", [](py::dict d, uintptr_t s) {
+    const auto a = patch_args(d);
+    py::gil_scoped_release nogil;
+    chk(patchify(a, S(s)), "patchify");
+  });
+  m.def("embed_tokens", [](py::dict d, uintptr_t s) {
+    const auto a = embed_args(d);
+    py::gil_scoped_release nogil;
+    chk(embed_tokens(a, S(s)), "embed_tokens");
+  });
+  m.def("layernorm", [](py::dict d, uintptr_t s) {
+    const auto a = ln_args(d);
+    py::gil_scoped_release nogil;
+    chk(layernorm(a, S(s)), "layernorm");
+  });
+  m.def("attention", [](py::dict d, uintptr_t s) {
+    const auto a = attn_args(d);
+    py::gil_scoped_release nogil;
+    chk(attention(a, S(s)), "attention");
+  });
   m.def("fc_mfma", [](py::dict d, uintptr_t s) {
     const auto a = fcm_args(d);
     py::gil_scoped_release nogil;
@@ -194,6 +244,18 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_fc", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_FC; op.name = name; op.fc = fc_args(d); p.add(op);
+      })
+      .def("add_patchify", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_PATCHIFY; op.name = name; op.pt = patch_args(d); p.add(op);
+      })
+      .def("add_embed", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_EMBED; op.name = name; op.em = embed_args(d); p.add(op);
+      })
+      .def("add_layernorm", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_LN; op.name = name; op.ln = ln_args(d); p.add(op);
+      })
+      .def("add_attention", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_ATTN; op.name = name; op.at = attn_args(d); p.add(op);
       })
       .def("add_fc_mfma", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_FC_MFMA; op.name = name; op.fcm = fcm_args(d); p.add(op);

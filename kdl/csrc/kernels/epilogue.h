@@ -11,12 +11,23 @@ namespace kdl {
 __device__ __forceinline__ long out_offset(const ConvGemmArgs& a, int m) {
   if (!a.opad) return (long)m * a.ldy;
   const int OHW = a.OH * a.OW;
+  if (a.opad == 2) {
+    const int b = m / OHW;
+    return ((long)b * (OHW + 1) + 1 + (m - b * OHW)) * a.ldy;
+  }
   const int b = m / OHW, rem = m - b * OHW;
   const int oh = rem / a.OW, ow = rem - oh * a.OW;
   return (((long)b * (a.OH + 2) + oh + 1) * (a.OW + 2) + ow + 1) * a.ldy;
 }
 
-// v: 8 bf16 (bias + optional pre-residual ReLU already applied) for row m, cols n..n+7
+// pre-residual activation of the fp32 accumulator + bias (relu_out 1 = ReLU, 3 = exact GELU)
+__device__ __forceinline__ float act_pre(int mode, float v) {
+  if (mode == 1) return fmaxf(v, 0.f);
+  if (mode == 3) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  return v;
+}
+
+// v: 8 bf16 (bias + optional pre-residual activation already applied) for row m, cols n..n+7
 __device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u32x4 v) {
   if (a.res) {
     const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);

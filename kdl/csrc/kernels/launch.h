@@ -24,9 +24,11 @@ struct ConvGemmArgs {
   int nstore;            // output channels written (<= ldy)
   int stride;            // spatial stride (MODE_PW / MODE_CONV)
   int relu_in;
-  int relu_out;          // 0 none; 1 ReLU before the residual add (Xception); 2 after it (ResNet)
+  int relu_out;          // 0 none; 1 ReLU before the residual add (Xception); 2 after it (ResNet);
+                         // 3 exact GELU before the residual add (ViT MLP)
   int opad;              // 1: write into the interior of a 1-pixel zero-bordered output buffer, so the
-                         //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks
+                         //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
+                         // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
@@ -109,6 +111,48 @@ struct FcMfmaArgs {
   int B, F, N, NF, relu;
 };
 hipError_t fc_mfma(const FcMfmaArgs& a, hipStream_t s);
+
+// ViT patch embedding input: uint8 NHWC image -> A [B*np][3*P*P] bf16, k = c*P*P + ky*P + kx,
+// normalised on load (per-channel scale/shift).
+struct PatchifyArgs {
+  const uint8_t* x;
+  uint16_t* y;
+  int B, H, W, P, ldy;
+  float scale[3], shift[3];
+};
+hipError_t patchify(const PatchifyArgs& a, hipStream_t s);
+
+// Token finalise: x [B][T][D] bf16 (rows 1..T-1 = patch embeddings); row 0 := cls + pos[0],
+// rows t >= 1 += pos[t]. cls [D], pos [T][D] fp32.
+struct EmbedArgs {
+  uint16_t* x;
+  const float* cls;
+  const float* pos;
+  int B, T, D;
+};
+hipError_t embed_tokens(const EmbedArgs& a, hipStream_t s);
+
+// LayerNorm over the last dim (D <= 2048): y[r][:D] = LN(x[r*ldx .. +D]) * gamma + beta, bf16.
+struct LnArgs {
+  const uint16_t* x;
+  uint16_t* y;
+  const float* gamma;
+  const float* beta;
+  long rows;
+  int D, ldx, ldy;
+  float eps;
+};
+hipError_t layernorm(const LnArgs& a, hipStream_t s);
+
+// Multi-head self-attention (flash-style, online softmax) over a packed QKV buffer:
+// qkv [B*T][3*H*dh] bf16 (q | k | v, head-major inside each), out [B*T][H*dh] bf16.
+struct AttnArgs {
+  const uint16_t* qkv;
+  uint16_t* out;
+  int B, T, H, dh;        // dh = 64
+  float scale;            // 1/sqrt(dh)
+};
+hipError_t attention(const AttnArgs& a, hipStream_t s);
 
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {

@@ -20,6 +20,10 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_GAP: return gap(op.gp, s);
     case OP_FC: return fc(op.fc, s);
     case OP_FC_MFMA: return fc_mfma(op.fcm, s);
+    case OP_PATCHIFY: return patchify(op.pt, s);
+    case OP_EMBED: return embed_tokens(op.em, s);
+    case OP_LN: return layernorm(op.ln, s);
+    case OP_ATTN: return attention(op.at, s);
   }
   return hipErrorInvalidValue;
 }

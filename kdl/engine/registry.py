@@ -41,7 +41,17 @@ def _resnet50():
                      R.resnet_forward)
 
 
-_FACTORIES = {"xception": _xception, "resnet50": _resnet50}
+def _vit_b16():
+    from ..models import vit as V
+    from .vit import ViTEngine
+    return ModelInfo("vit_b16", V.INPUT_SIZE, 1000, V.TOTAL_PARAMS,
+                     "ViT-B/16 224x224 (torchvision layout, 86,567,656 params)",
+                     lambda seed=0: V.init_params(seed=seed),
+                     lambda p, max_batch, device, **kw: ViTEngine(p, max_batch=max_batch, device=device, **kw),
+                     V.vit_forward)
+
+
+_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "vit_b16": _vit_b16}
 
 
 def models() -> list[str]:

@@ -87,3 +87,12 @@ def test_resnet50_oracle_shapes_and_cost():
     y1, y2 = R.resnet_forward(p, x), R.resnet_forward(p, x)
     assert y1.shape == (1, 1000) and torch.equal(y1, y2)
     assert [b.stride for b in R.blocks()].count(2) == 3          # v1.5: stride on conv2 of 3 stages
+
+
+def test_vit_b16_oracle_shapes_and_cost():
+    from kdl.models import vit as V
+    assert V.count_params() == V.TOTAL_PARAMS == 86_567_656     # torchvision vit_b_16
+    assert abs(V.macs_per_image() / 1e9 - 17.56) < 0.01
+    p = V.init_params(seed=1)
+    x = torch.randint(0, 256, (1, 224, 224, 3), dtype=torch.uint8)
+    assert V.vit_forward(p, x).shape == (1, 1000)
