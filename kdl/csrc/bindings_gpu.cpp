@@ -101,6 +101,27 @@ AttnArgs attn_args(const py::dict& d) {
   a.scale = F(d, "scale", 0.125f);
   return a;
 }
+DwkArgs dwk_args(const py::dict& d) {
+  DwkArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.w = P<const float>(d, "w"); a.bias = P<const float>(d, "bias");
+  a.y = P<uint16_t>(d, "y"); a.pool = P<float>(d, "pool"); a.w1 = P<const float>(d, "w1");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.C = I(d, "C"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
+  a.K = I(d, "K"); a.S = I(d, "S", 1); a.pad = I(d, "pad"); a.act = I(d, "act"); a.Cs = I(d, "Cs");
+  return a;
+}
+SeArgs se_args(const py::dict& d) {
+  SeArgs a{};
+  a.pool = P<const float>(d, "pool"); a.b1 = P<const float>(d, "b1");
+  a.w2t = P<const float>(d, "w2t"); a.b2 = P<const float>(d, "b2"); a.scale = P<float>(d, "scale");
+  a.B = I(d, "B"); a.ntiles = I(d, "ntiles"); a.HW = I(d, "HW"); a.C = I(d, "C"); a.Cs = I(d, "Cs");
+  return a;
+}
+ChScaleArgs chs_args(const py::dict& d) {
+  ChScaleArgs a{};
+  a.y = P<uint16_t>(d, "y"); a.scale = P<const float>(d, "scale");
+  a.B = I(d, "B"); a.HW = I(d, "HW"); a.C = I(d, "C");
+  return a;
+}
 FcMfmaArgs fcm_args(const py::dict& d) {
   FcMfmaArgs a{};
   a.xb = P<const uint16_t>(d, "xb"); a.wp = P<const uint16_t>(d, "wp"); a.bias = P<const float>(d, "bias");
@@ -208,6 +229,27 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(attention(a, S(s)), "attention");
   });
+  m.def("dwk", [](py::dict d, uintptr_t s) {
+    const auto a = dwk_args(d);
+    py::gil_scoped_release nogil;
+    chk(dwk(a, S(s)), "dwk");
+  });
+  m.def("dwk_tiles", [](py::dict d) {
+    const auto a = dwk_args(d);
+    int cg, rb, tw, nt;
+    dwk_tiles(a, &cg, &rb, &tw, &nt);
+    return py::make_tuple(cg, rb, tw, nt);
+  });
+  m.def("squeeze_excite", [](py::dict d, uintptr_t s) {
+    const auto a = se_args(d);
+    py::gil_scoped_release nogil;
+    chk(squeeze_excite(a, S(s)), "squeeze_excite");
+  });
+  m.def("channel_scale", [](py::dict d, uintptr_t s) {
+    const auto a = chs_args(d);
+    py::gil_scoped_release nogil;
+    chk(channel_scale(a, S(s)), "channel_scale");
+  });
   m.def("fc_mfma", [](py::dict d, uintptr_t s) {
     const auto a = fcm_args(d);
     py::gil_scoped_release nogil;
@@ -256,6 +298,15 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_attention", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_ATTN; op.name = name; op.at = attn_args(d); p.add(op);
+      })
+      .def("add_dwk", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_DWK; op.name = name; op.dk = dwk_args(d); p.add(op);
+      })
+      .def("add_se", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_SE; op.name = name; op.se = se_args(d); p.add(op);
+      })
+      .def("add_chscale", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_CHSCALE; op.name = name; op.cs = chs_args(d); p.add(op);
       })
       .def("add_fc_mfma", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_FC_MFMA; op.name = name; op.fcm = fcm_args(d); p.add(op);

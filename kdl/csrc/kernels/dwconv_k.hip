@@ -1,0 +1,280 @@
+// MBConv depthwise KxK conv (K = 3/5, stride 1/2, symmetric pad) + folded BN bias
+// + SiLU, NHWC bf16, with the squeeze-excite average pool AND the squeeze FC fused
+// in: each tile reduces its channel sums and projects them on w1 (fc1 is linear in
+// the mean), leaving only bias + SiLU + fc2 + sigmoid for se_kernel (SURVEY.md §2.6 EfficientNet-B7: "dw 5x5 (+stride
+// 2), squeeze-excite ... SiLU epilogue"; the 600x600 large-activation path).
+//
+// Same tiling as dw3x3_tile_kernel (dwconv.hip): block = image x RB output rows x
+// TW output columns x CG 8-channel chunks; the ((RB-1)S+K) x ((TW-1)S+K) input
+// patch is staged once into LDS with all of a thread's loads in flight together;
+// an item = (chunk, row, SEG-column segment) slides a register window along W.
+// SE partial sums are reduced in a fixed order (deterministic, no atomics):
+// CG divides 256, so every item of a thread has the same chunk.
+#include "common.h"
+#include "launch.h"
+
+namespace kdl {
+
+constexpr int DWK_MAXL = 8;
+
+__device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
+
+template <int K, int S, int SEG>
+__global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int TW) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int C8 = a.C >> 3;
+  const int ngroups = C8 / CG;
+  const int nbands = (a.OH + RB - 1) / RB;
+  const int ncolt = (a.OW + TW - 1) / TW;
+  int bid = blockIdx.x;
+  const int g = bid % ngroups;
+  bid /= ngroups;
+  const int ct = bid % ncolt;
+  bid /= ncolt;
+  const int band = bid % nbands;
+  const int b = bid / nbands;
+  const int h0 = band * RB, c0 = ct * TW;
+  const int PR = (RB - 1) * S + K, PC = (TW - 1) * S + K;
+  const int ih0 = h0 * S - a.pad, iw0 = c0 * S - a.pad;
+  const int tid = threadIdx.x;
+  const int cbase = g * CG;
+
+  float* wsm = (float*)dsm;                                 // [K*K][CG*8]
+  uint8_t* xsm = dsm + K * K * CG * 8 * 4;                  // [PR][PC][CG][16B]
+  for (int i = tid; i < K * K * CG * 2; i += 256) {
+    const int tap = i / (CG * 2), rem = i - tap * CG * 2;
+    const int c = rem >> 1, half = rem & 1;
+    *(float4*)(wsm + tap * CG * 8 + c * 8 + half * 4) = *(const float4*)(a.w + tap * a.C + (cbase + c) * 8 + half * 4);
+  }
+  const int nst = PR * PC * CG;
+  const int dc = 256 % CG, dt = 256 / CG;
+  const int dcol = dt % PC, dr = dt / PC;
+  int c = tid % CG, t = tid / CG;
+  int col = t % PC, r = t / PC;
+  const long img = (long)b * a.H;
+  for (int base = 0; base < nst; base += 256 * DWK_MAXL) {
+    u32x4 v[DWK_MAXL];
+    int cc[DWK_MAXL], cl[DWK_MAXL], rr[DWK_MAXL];
+#pragma unroll
+    for (int l = 0; l < DWK_MAXL; ++l) {
+      cc[l] = c; cl[l] = col; rr[l] = r;
+      v[l] = (u32x4){0u, 0u, 0u, 0u};
+      const int ih = ih0 + r, iw = iw0 + col;
+      if (base + tid + l * 256 < nst && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        v[l] = *(const u32x4*)(a.x + ((img + ih) * a.W + iw) * a.C + (cbase + c) * 8);
+      c += dc;
+      int carry = c >= CG;
+      c -= carry ? CG : 0;
+      col += dcol + carry;
+      carry = col >= PC;
+      col -= carry ? PC : 0;
+      r += dr + carry;
+    }
+#pragma unroll
+    for (int l = 0; l < DWK_MAXL; ++l)
+      if (base + tid + l * 256 < nst) *(u32x4*)(xsm + (((long)rr[l] * PC + cl[l]) * CG + cc[l]) * 16) = v[l];
+  }
+  __syncthreads();
+
+  const int nseg = (TW + SEG - 1) / SEG;
+  const int nitems = CG * RB * nseg;
+  const int ic = tid % CG;                 // CG divides 256: fixed chunk per thread
+  const float4 bz0 = *(const float4*)(a.bias + (cbase + ic) * 8);
+  const float4 bz1 = *(const float4*)(a.bias + (cbase + ic) * 8 + 4);
+  const float bias[8] = {bz0.x, bz0.y, bz0.z, bz0.w, bz1.x, bz1.y, bz1.z, bz1.w};
+  float psum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int it = tid; it < nitems; it += 256) {
+    const int tt = it / CG;
+    const int s = tt % nseg, ir = tt / nseg;
+    const int w0 = s * SEG;
+    if (h0 + ir >= a.OH || c0 + w0 >= a.OW) continue;
+    f32x2 acc[SEG][4];
+#pragma unroll
+    for (int o = 0; o < SEG; ++o)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) acc[o][d] = (f32x2){0.f, 0.f};
+    // dy stays a rolled loop: unrolled, hipcc hoists all K*K taps' weights out of
+    // the item loop (200 VGPRs at K=5 -> 512 VGPRs + scratch spills)
+#pragma unroll 1
+    for (int dy = 0; dy < K; ++dy) {
+      f32x2 wt[K][4];
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        const float* wp = wsm + (dy * K + dx) * CG * 8 + ic * 8;
+        const float4 p = *(const float4*)wp;
+        const float4 q = *(const float4*)(wp + 4);
+        wt[dx][0] = (f32x2){p.x, p.y};
+        wt[dx][1] = (f32x2){p.z, p.w};
+        wt[dx][2] = (f32x2){q.x, q.y};
+        wt[dx][3] = (f32x2){q.z, q.w};
+      }
+      const uint8_t* rowp = xsm + ((long)(ir * S + dy) * PC * CG + ic) * 16;
+#pragma unroll
+      for (int j = 0; j < (SEG - 1) * S + K; ++j) {
+        const int lc = min(w0 * S + j, PC - 1);   // clamping only feeds outputs that are not stored
+        const u32x4 v = *(const u32x4*)(rowp + (long)lc * CG * 16);
+        f32x2 xv[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) xv[d] = (f32x2){bf_lo(v[d]), bf_hi(v[d])};
+#pragma unroll
+        for (int o = 0; o < SEG; ++o) {
+          const int dx = j - o * S;
+          if (dx >= 0 && dx < K) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) acc[o][d] = __builtin_elementwise_fma(xv[d], wt[dx][d], acc[o][d]);
+          }
+        }
+      }
+    }
+    uint16_t* yb = a.y + (((long)b * a.OH + h0 + ir) * a.OW + c0 + w0) * a.C + (cbase + ic) * 8;
+    const int lim = min(SEG, min(TW - w0, a.OW - c0 - w0));
+#pragma unroll
+    for (int o = 0; o < SEG; ++o) {
+      if (o < lim) {
+        float f[8];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          f[2 * d] = acc[o][d][0] + bias[2 * d];
+          f[2 * d + 1] = acc[o][d][1] + bias[2 * d + 1];
+        }
+        u32x4 out;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          if (a.act == 2) {
+            f[2 * d] = silu(f[2 * d]);
+            f[2 * d + 1] = silu(f[2 * d + 1]);
+          }
+          out[d] = pack_bf16(f[2 * d], f[2 * d + 1]);
+          // the SE pool sees exactly the stored (bf16-rounded) activations
+          psum[2 * d] += bf_lo(out[d]);
+          psum[2 * d + 1] += bf_hi(out[d]);
+        }
+        *(u32x4*)(yb + (long)o * a.C) = out;
+      }
+    }
+  }
+  if (a.pool) {
+    __syncthreads();                       // staging image no longer needed
+    float* red = (float*)dsm;              // [256][8]
+#pragma unroll
+    for (int d = 0; d < 8; ++d) red[tid * 8 + d] = psum[d];
+    __syncthreads();
+    float sum = 0.f;
+    if (tid < CG * 8) {
+      const int rc = tid >> 3, d = tid & 7;
+      for (int u = rc; u < 256; u += CG) sum += red[u * 8 + d];
+    }
+    __syncthreads();
+    float* csum = red + 256 * 8;             // [CG*8] channel sums of this tile
+    if (tid < CG * 8) csum[tid] = sum;
+    __syncthreads();
+    // squeeze FC fused: this tile's contribution to h[j] = sum_c w1[j][c] * mean[c]
+    // (the mean is linear in the tiles' sums; se_kernel adds the parts up)
+    const int part = (band * ncolt + ct) * ngroups + g;
+    const int nparts = nbands * ncolt * ngroups;
+    for (int j = tid; j < a.Cs; j += 256) {
+      const float* w1 = a.w1 + (long)j * a.C + cbase * 8;
+      float h = 0.f;
+      for (int cc8 = 0; cc8 < CG * 8; ++cc8) h += w1[cc8] * csum[cc8];
+      a.pool[((long)b * nparts + part) * a.Cs + j] = h;
+    }
+  }
+}
+
+static size_t dwk_smem(int K, int S, int CG, int RB, int TW) {
+  const size_t patch = (size_t)((RB - 1) * S + K) * ((TW - 1) * S + K) * CG * 16;
+  const size_t w = (size_t)K * K * CG * 8 * 4;
+  const size_t red = (256 * 8 + 64) * 4;
+  return w + patch > red ? w + patch : red;
+}
+
+// Tile choice: column tiles of <= 48 outputs; for each power-of-two chunk group
+// CG dividing C/8 the tallest row band that fits 96 KiB of LDS; keep the CG with
+// the tallest band (halo re-reads (RB-1)S+K over RB*S rows), ties -> wider CG.
+void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles) {
+  const int C8 = a.C / 8;
+  const int ncol = (a.OW + 47) / 48;
+  const int TW = (a.OW + ncol - 1) / ncol;
+  int bestcg = 1, bestrb = 0;
+  for (int CG : {8, 4, 2, 1}) {
+    if (C8 % CG != 0) continue;
+    int RB = 1;
+    while (RB < a.OH && RB < 16 && dwk_smem(a.K, a.S, CG, RB + 1, TW) <= 96 * 1024) ++RB;
+    if (dwk_smem(a.K, a.S, CG, RB, TW) > 96 * 1024) continue;
+    if (RB > bestrb) { bestrb = RB; bestcg = CG; }
+  }
+  if (bestrb == 0) bestrb = 1;
+  *cg = bestcg; *rb = bestrb; *tw = TW;
+  *ntiles = ((a.OH + bestrb - 1) / bestrb) * ((a.OW + TW - 1) / TW) * ((a.C / 8) / bestcg);
+}
+
+hipError_t dwk(const DwkArgs& a, hipStream_t s) {
+  if (a.C % 8 != 0 || a.B <= 0 || (a.K != 3 && a.K != 5) || (a.S != 1 && a.S != 2)) return hipErrorInvalidValue;
+  int CG, RB, TW, nt;
+  dwk_tiles(a, &CG, &RB, &TW, &nt);
+  const size_t smem = dwk_smem(a.K, a.S, CG, RB, TW);
+  if (smem > 160 * 1024) return hipErrorInvalidValue;
+  const long nblk = (long)a.B * nt;          // nt counts (row band, column tile, channel group)
+  const dim3 grid((unsigned)nblk), block(256);
+#define KDL_DWK(k, st) \
+  if (a.K == k && a.S == st) { hipLaunchKernelGGL((dwk_kernel<k, st, 4>), grid, block, smem, s, a, CG, RB, TW); return hipGetLastError(); }
+  KDL_DWK(3, 1) KDL_DWK(3, 2) KDL_DWK(5, 1) KDL_DWK(5, 2)
+#undef KDL_DWK
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------- squeeze-excite
+// grid (image, 256-channel slice): every block re-sums the tiles' fc1 parts (tiny),
+// applies bias + SiLU, then its 256 channels run fc2 with the TRANSPOSED w2 ([Cs][C]:
+// coalesced across threads, independent loads) and the sigmoid.
+__global__ __launch_bounds__(256) void se_kernel(SeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hid[];   // [Cs]
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float inv = 1.f / (float)a.HW;
+  for (int j = tid; j < a.Cs; j += 256) {
+    float h = 0.f;
+    for (int t = 0; t < a.ntiles; ++t) h += a.pool[((long)b * a.ntiles + t) * a.Cs + j];
+    h = h * inv + a.b1[j];
+    hid[j] = silu(h);
+  }
+  __syncthreads();
+  const int c = blockIdx.y * 256 + tid;
+  if (c < a.C) {
+    float s = a.b2[c];
+#pragma unroll 8
+    for (int j = 0; j < a.Cs; ++j) s += a.w2t[(long)j * a.C + c] * hid[j];
+    a.scale[(long)b * a.C + c] = 1.f / (1.f + __expf(-s));
+  }
+}
+
+hipError_t squeeze_excite(const SeArgs& a, hipStream_t s) {
+  const size_t smem = (size_t)a.Cs * sizeof(float);
+  if (a.B <= 0 || a.Cs <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(se_kernel, dim3(a.B, (a.C + 255) / 256), dim3(256), smem, s, a);
+  return hipGetLastError();
+}
+
+// y[b][p][c] *= scale[b][c] (in place, 16-byte vectors)
+__global__ __launch_bounds__(256) void chscale_kernel(ChScaleArgs a) {
+  const int C8 = a.C / 8;
+  const long total = (long)a.B * a.HW * C8;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c8 = (int)(i % C8);
+  const int b = (int)(i / ((long)a.HW * C8));
+  uint16_t* p = a.y + i * 8;
+  const float* sc = a.scale + (long)b * a.C + c8 * 8;
+  u32x4 v = *(const u32x4*)p;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) v[d] = pack_bf16(bf_lo(v[d]) * sc[2 * d], bf_hi(v[d]) * sc[2 * d + 1]);
+  *(u32x4*)p = v;
+}
+
+hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s) {
+  if (a.C % 8 != 0) return hipErrorInvalidValue;
+  const long total = (long)a.B * a.HW * (a.C / 8);
+  hipLaunchKernelGGL(chscale_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace kdl

@@ -20,10 +20,11 @@ __device__ __forceinline__ long out_offset(const ConvGemmArgs& a, int m) {
   return (((long)b * (a.OH + 2) + oh + 1) * (a.OW + 2) + ow + 1) * a.ldy;
 }
 
-// pre-residual activation of the fp32 accumulator + bias (relu_out 1 = ReLU, 3 = exact GELU)
+// pre-residual activation of the fp32 accumulator + bias (relu_out 1 ReLU, 3 exact GELU, 4 SiLU)
 __device__ __forceinline__ float act_pre(int mode, float v) {
   if (mode == 1) return fmaxf(v, 0.f);
   if (mode == 3) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  if (mode == 4) return v / (1.f + __expf(-v));
   return v;
 }
 

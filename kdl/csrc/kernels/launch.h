@@ -25,7 +25,7 @@ struct ConvGemmArgs {
   int stride;            // spatial stride (MODE_PW / MODE_CONV)
   int relu_in;
   int relu_out;          // 0 none; 1 ReLU before the residual add (Xception); 2 after it (ResNet);
-                         // 3 exact GELU before the residual add (ViT MLP)
+                         // 3 exact GELU before the residual add (ViT MLP); 4 SiLU before it (EfficientNet)
   int opad;              // 1: write into the interior of a 1-pixel zero-bordered output buffer, so the
                          //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
                          // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
@@ -68,7 +68,7 @@ struct StemArgs {
   int KH, KW, stride, pad, cout;  // generic KxK stride/pad conv from 3 channels (cout = 32 or 64)
   float scale[3], shift[3];       // per-channel input normalisation applied on load (zero padding
                                   // stays exact: padded taps are 0 in the normalised space)
-  int relu;
+  int relu;                       // 0 none, 1 ReLU, 2 SiLU
 };
 hipError_t stem_conv(const StemArgs& a, hipStream_t s);
 
@@ -153,6 +153,40 @@ struct AttnArgs {
   float scale;            // 1/sqrt(dh)
 };
 hipError_t attention(const AttnArgs& a, hipStream_t s);
+
+// MBConv depthwise KxK (K 3/5, stride S 1/2, symmetric pad) + bias (+SiLU) with the SE
+// average pool and squeeze FC fused: pool[b][part][Cs] = sum over the part's channels of
+// w1[j][c] * (sum of the part's outputs of channel c); part = (band, column tile, group).
+struct DwkArgs {
+  const uint16_t* x;      // [B][H][W][C]
+  const float* w;         // [K*K][C] fp32 (BN scale folded)
+  const float* bias;      // [C]
+  uint16_t* y;            // [B][OH][OW][C]
+  float* pool;            // null: no SE
+  const float* w1;        // SE fc1 [Cs][C]
+  int B, H, W, C, OH, OW, K, S, pad, act;   // act: 0 none, 2 SiLU
+  int Cs;
+};
+hipError_t dwk(const DwkArgs& a, hipStream_t s);
+void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles);
+
+// Squeeze-excite tail: scale[b][c] = sigmoid(W2 SiLU(sum_parts pool / HW + b1) + b2).
+struct SeArgs {
+  const float* pool;      // [B][ntiles][Cs] fc1 partials from dwk
+  const float* b1;        // [Cs]
+  const float* w2t;       // [Cs][C] (fc2 transposed)
+  const float* b2;        // [C]
+  float* scale;           // [B][C]
+  int B, ntiles, HW, C, Cs;
+};
+hipError_t squeeze_excite(const SeArgs& a, hipStream_t s);
+
+struct ChScaleArgs {
+  uint16_t* y;            // [B][HW][C] bf16, scaled in place
+  const float* scale;     // [B][C]
+  int B, HW, C;
+};
+hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s);
 
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {

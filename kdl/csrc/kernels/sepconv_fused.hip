@@ -207,7 +207,7 @@ __global__ __launch_bounds__(64 * NW) void sepconv_fused_kernel(ConvGemmArgs a, 
       const int ml = i * 16 + col;
       float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y;
       float v2 = acc[i][j][2] + bv.z, v3 = acc[i][j][3] + bv.w;
-      if (a.relu_out == 1 || a.relu_out == 3) {
+      if (a.relu_out == 1 || a.relu_out >= 3) {
         v0 = act_pre(a.relu_out, v0); v1 = act_pre(a.relu_out, v1);
         v2 = act_pre(a.relu_out, v2); v3 = act_pre(a.relu_out, v3);
       }

@@ -90,8 +90,11 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
         const float4 bv = *(const float4*)(a.bias + n);
         float v0 = acc[f][j][0] + bv.x, v1 = acc[f][j][1] + bv.y;
         float v2 = acc[f][j][2] + bv.z, v3 = acc[f][j][3] + bv.w;
-        if (a.relu) {
+        if (a.relu == 1) {
           v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        } else if (a.relu == 2) {
+          v0 = v0 / (1.f + __expf(-v0)); v1 = v1 / (1.f + __expf(-v1));
+          v2 = v2 / (1.f + __expf(-v2)); v3 = v3 / (1.f + __expf(-v3));
         }
         *(u32x2*)(a.y + (long)mo * a.ldy + n) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
       }

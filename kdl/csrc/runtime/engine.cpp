@@ -24,6 +24,9 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_EMBED: return embed_tokens(op.em, s);
     case OP_LN: return layernorm(op.ln, s);
     case OP_ATTN: return attention(op.at, s);
+    case OP_DWK: return dwk(op.dk, s);
+    case OP_SE: return squeeze_excite(op.se, s);
+    case OP_CHSCALE: return channel_scale(op.cs, s);
   }
   return hipErrorInvalidValue;
 }

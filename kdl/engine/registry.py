@@ -51,7 +51,19 @@ def _vit_b16():
                      V.vit_forward)
 
 
-_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "vit_b16": _vit_b16}
+def _efficientnet_b7():
+    from ..models import efficientnet as E
+    from .efficientnet import EfficientNetEngine
+    return ModelInfo("efficientnet_b7", E.INPUT_SIZE, 1000, E.TOTAL_PARAMS,
+                     "EfficientNet-B7 600x600 (torchvision layout, 66,347,960 params)",
+                     lambda seed=0: E.init_params(seed=seed),
+                     lambda p, max_batch, device, **kw: EfficientNetEngine(p, max_batch=max_batch, device=device,
+                                                                           **kw),
+                     E.efficientnet_forward)
+
+
+_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "vit_b16": _vit_b16,
+              "efficientnet_b7": _efficientnet_b7}
 
 
 def models() -> list[str]:

@@ -1,0 +1,69 @@
+"""EfficientNet-B7 on MI355X: KxK/stride depthwise + SiLU with the fused SE pool,
+the squeeze-excite MLP, channel scale and SiLU epilogues against fp32 torch, then
+the engine vs the oracle (at 256x256 to keep the fp32 CPU oracle quick)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from kdl.models import efficientnet as E
+from kdl.ops import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a.float().cpu() - b.float().cpu()).abs().max() / b.float().abs().max()).item()
+
+
+@pytest.mark.parametrize("K,S,H,C", [(3, 1, 37, 64), (3, 2, 75, 288), (5, 1, 19, 1344), (5, 2, 150, 192),
+                                     (5, 2, 38, 960)])
+def test_dwk_silu_and_fused_squeeze_excite(K, S, H, C):
+    gen = torch.Generator().manual_seed(K * 100 + S * 10 + H)
+    B, Cs = 2, max(1, C // 24)
+    pad = (K - 1) // 2
+    OH = (H + 2 * pad - K) // S + 1
+    x = torch.randn(B, H, H, C, generator=gen).to(torch.bfloat16)
+    w = torch.randn(C, 1, K, K, generator=gen) / K
+    bias = torch.randn(C, generator=gen) * 0.1
+    w1, b1 = torch.randn(Cs, C, generator=gen) / C ** 0.5, torch.randn(Cs, generator=gen) * 0.1
+    w2, b2 = torch.randn(C, Cs, generator=gen) / Cs ** 0.5, torch.randn(C, generator=gen) * 0.1
+    wk = w[:, 0].permute(1, 2, 0).reshape(K * K, C).contiguous()
+    y = torch.zeros(B, OH, OH, C, dtype=torch.bfloat16, device=DEV)
+    C_ = _lib.lib()
+    args = dict(B=B, H=H, W=H, C=C, OH=OH, OW=OH, K=K, S=S, pad=pad, Cs=Cs)
+    nt = C_.dwk_tiles(args)[3]
+    pool = torch.zeros(B, nt, Cs, device=DEV)
+    scale = torch.zeros(B, C, device=DEV)
+    d = {k: v.to(DEV).contiguous() for k, v in dict(x=x, w=wk, bias=bias, w1=w1, b1=b1, w2t=w2.t(), b2=b2).items()}
+    s = _lib.stream_ptr()
+    C_.dwk(dict(args, x=d["x"].data_ptr(), w=d["w"].data_ptr(), bias=d["bias"].data_ptr(), y=y.data_ptr(),
+                pool=pool.data_ptr(), w1=d["w1"].data_ptr(), act=2), s)
+    C_.squeeze_excite(dict(pool=pool.data_ptr(), b1=d["b1"].data_ptr(), w2t=d["w2t"].data_ptr(),
+                           b2=d["b2"].data_ptr(), scale=scale.data_ptr(), B=B, ntiles=nt, HW=OH * OH, C=C,
+                           Cs=Cs), s)
+    y0 = y.clone()
+    C_.channel_scale(dict(y=y.data_ptr(), scale=scale.data_ptr(), B=B, HW=OH * OH, C=C), s)
+    torch.cuda.synchronize()
+    ref = F.silu(F.conv2d(x.float().permute(0, 3, 1, 2), w, bias, stride=S, padding=pad, groups=C)).permute(0, 2, 3, 1)
+    assert _rel(y0, ref) < 2e-2
+    m = y0.float().cpu().mean(dim=(1, 2))                      # the pool sees the stored activations
+    sref = torch.sigmoid(F.silu(m @ w1.t() + b1) @ w2.t() + b2)
+    assert _rel(scale, sref) < 1e-3
+    assert _rel(y, y0.float() * scale[:, None, None, :]) < 1e-2
+
+
+def test_efficientnet_engine_matches_oracle():
+    from kdl.engine.efficientnet import EfficientNetEngine
+    S = 256
+    p = E.init_params(seed=0, calib_size=S)
+    eng = EfficientNetEngine(p, max_batch=2, device=DEV, size=S)
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randint(0, 256, (2, S, S, 3), generator=gen, dtype=torch.uint8)
+    ref = E.efficientnet_forward(p, x)
+    for capture in (False, True):
+        out = eng.forward(x.to(DEV), capture=capture).cpu()
+        cos = F.cosine_similarity(out, ref, dim=1)
+        # a plain torch bf16 forward of the same oracle measures cosine 0.945 / 0.980 on these two
+        # images (55 blocks of bf16 drift); the fused engine keeps fp32 accumulators throughout
+        assert cos.min() > 0.96, cos

@@ -96,3 +96,11 @@ def test_vit_b16_oracle_shapes_and_cost():
     p = V.init_params(seed=1)
     x = torch.randint(0, 256, (1, 224, 224, 3), dtype=torch.uint8)
     assert V.vit_forward(p, x).shape == (1, 1000)
+
+
+def test_efficientnet_b7_oracle_shapes_and_cost():
+    from kdl.models import efficientnet as E
+    assert len(E.blocks()) == 55
+    assert E.count_params() == E.TOTAL_PARAMS == 66_347_960   # torchvision efficientnet_b7
+    assert abs(E.macs_per_image() / 1e9 - 37.75) < 0.01
+    assert (E.STEM, E.HEAD) == (64, 2560)
