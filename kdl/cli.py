@@ -2,7 +2,9 @@
 
   show <saved_model_dir>                     saved_model_cli-style signature dump (guide.md:202)
   convert-savedmodel <saved_model_dir> <out> SavedModel -> kdl_params.safetensors + kdl_model.json
-  make-synthetic <repo>/<version> [--seed]   random-init SavedModel of the exact architecture
+  make-synthetic <repo>/<version> [--seed] [--model xception|resnet50|vit_b16|efficientnet_b7]
+                                             random-init weights of the exact architecture (Xception:
+                                             a SavedModel; other families: torchvision-layout safetensors)
   serve [server flags...]                    same as python -m kdl.serving
 """
 from __future__ import annotations
@@ -25,6 +27,7 @@ def main(argv=None) -> int:
     m.add_argument("dst")
     m.add_argument("--seed", type=int, default=0)
     m.add_argument("--residual-offset", type=int, default=0)
+    m.add_argument("--model", default="xception")
     sv = sub.add_parser("serve")
     sv.add_argument("rest", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
@@ -48,6 +51,18 @@ def main(argv=None) -> int:
         (out / "kdl_model.json").write_text(json.dumps(meta, indent=1))
         print(f"wrote {out}/kdl_params.safetensors ({len(params)} tensors)")
     elif a.cmd == "make-synthetic":
+        if a.model != "xception":
+            from safetensors.torch import save_file
+
+            from .engine import registry
+            info = registry.get(a.model)
+            dst = Path(a.dst)
+            dst.mkdir(parents=True, exist_ok=True)
+            params = {k: v.contiguous() for k, v in info.init_params(a.seed).items()}
+            save_file(params, str(dst / "kdl_params.safetensors"))
+            (dst / "kdl_model.json").write_text(json.dumps({"family": a.model}))
+            print(f"wrote synthetic {a.model} weights to {dst}")
+            return 0
         from .ingest.keras_map import to_keras_variables
         from .ingest.savedmodel import write_savedmodel
         from .models import xception as X

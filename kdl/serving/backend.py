@@ -6,12 +6,16 @@ copies the formed batch into pinned staging, H2D, replays the captured
 hipGraph of the bucket, D2H of the logits -> ``finish`` wakes the handlers.
 
 Backends:
-  * ``gpu``: ``kdl.engine.XceptionEngine`` (fused HIP kernels, hipGraph per
-    bucket), one executor per MI355X (data parallel over the node's GPUs: each
-    GPU pulls whole batches from the shared batcher, host-direct H2D over its
-    own PCIe link).
-  * ``cpu``: the fp32 Keras-semantics torch oracle ("config #1: plumbing, no
-    GPU").
+  * ``gpu``: the model family's MI355X engine (``kdl.engine.registry``: fused HIP
+    kernels, hipGraph per bucket), one executor per MI355X (data parallel over
+    the node's GPUs: each GPU pulls whole batches from the shared batcher,
+    host-direct H2D over its own PCIe link).
+  * ``cpu``: the family's fp32 torch oracle ("config #1: plumbing, no GPU").
+
+Families: ``xception`` (the reference's clothing model; SavedModel ingest,
+``serving_default`` = f32 ``input_8`` like TF-Serving, plus ``serving_uint8``),
+and ``resnet50`` / ``vit_b16`` / ``efficientnet_b7`` (BASELINE.json configs;
+torchvision-layout safetensors or synthetic weights, uint8 ``images`` input).
 """
 from __future__ import annotations
 
@@ -61,9 +65,25 @@ class SignatureInfo:
 class ModelSource:
     """Where a version's weights come from."""
     params: dict
-    head: X.Head
+    head: X.Head | None
     signatures: dict[str, SignatureInfo] = field(default_factory=dict)
     origin: str = ""
+    family: str = "xception"
+    input_size: int = IMG
+    classes: int = 10
+
+
+def _family_source(family: str, params: dict | None, seed: int, origin: str) -> ModelSource:
+    """Non-Xception families: uint8 NHWC images in, fp32 logits out."""
+    from ..engine import registry
+    info = registry.get(family)
+    if params is None:
+        params = info.init_params(seed)
+    S, n = info.input_size, info.classes
+    sigs = {name: SignatureInfo(name, NATIVE_INPUT_KEY, P.DT_UINT8, "logits", input_shape=(-1, S, S, 3),
+                                output_shape=(-1, n)) for name in ("serving_default", NATIVE_SIGNATURE)}
+    return ModelSource(params=params, head=None, signatures=sigs, origin=origin, family=family,
+                       input_size=S, classes=n)
 
 
 def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
@@ -86,15 +106,20 @@ def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
         from safetensors.torch import load_file
         params = load_file(str(path / "kdl_params.safetensors"))
         meta = json.loads((path / "kdl_model.json").read_text()) if (path / "kdl_model.json").exists() else {}
+        if meta.get("family", "xception") != "xception":
+            return _family_source(meta["family"], params, 0, "kdl_safetensors")
         head = X.Head(**meta.get("head", {}))
         for name, s in meta.get("signatures", {}).items():
             sigs[name] = SignatureInfo(name=name, input_key=s["input_key"], input_dtype=s.get("input_dtype", 1),
                                        output_key=s["output_key"])
         origin = "kdl_safetensors"
     elif synthetic or (path / "synthetic.json").exists():
-        seed = 0
+        seed, family = 0, "xception"
         if (path / "synthetic.json").exists():
-            seed = json.loads((path / "synthetic.json").read_text()).get("seed", 0)
+            meta = json.loads((path / "synthetic.json").read_text())
+            seed, family = meta.get("seed", 0), meta.get("model", "xception")
+        if family != "xception":
+            return _family_source(family, None, seed, f"synthetic({family}, seed={seed})")
         params, head = X.init_params(seed=seed), X.DEFAULT_HEAD
         origin = f"synthetic(seed={seed})"
     else:
@@ -102,8 +127,9 @@ def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
     if "serving_default" not in sigs:
         sigs["serving_default"] = SignatureInfo("serving_default", "input_8", P.DT_FLOAT, head.out)
     out_key = sigs["serving_default"].output_key
-    sigs.setdefault(NATIVE_SIGNATURE, SignatureInfo(NATIVE_SIGNATURE, NATIVE_INPUT_KEY, P.DT_UINT8, out_key))
-    return ModelSource(params=params, head=head, signatures=sigs, origin=origin)
+    sigs.setdefault(NATIVE_SIGNATURE, SignatureInfo(NATIVE_SIGNATURE, NATIVE_INPUT_KEY, P.DT_UINT8, out_key,
+                                                    output_shape=(-1, head.classes)))
+    return ModelSource(params=params, head=head, signatures=sigs, origin=origin, classes=head.classes)
 
 
 # ---------------------------------------------------------------------- executors
@@ -155,20 +181,27 @@ class GPUExecutor(_Executor):
         self.engine_kwargs = engine_kwargs
 
     def setup(self):
+        from ..engine import registry
         from ..engine.tuning import tuning_path
-        from ..engine.xception import XceptionEngine
         torch.cuda.set_device(self.device)
         r = self.runner
+        src = r.source
         bs = r.buckets
         in_kind = "u8" if r.sig.input_dtype == P.DT_UINT8 else "f32"
-        self.engine = XceptionEngine(r.source.params, max_batch=bs[-1], device=f"cuda:{self.device}",
-                                     in_kind=in_kind, head=r.source.head, buckets=bs)
-        tp = tuning_path("xception", bs[-1])
+        dev = f"cuda:{self.device}"
+        if src.family == "xception":
+            from ..engine.xception import XceptionEngine
+            self.engine = XceptionEngine(src.params, max_batch=bs[-1], device=dev, in_kind=in_kind,
+                                         head=src.head, buckets=bs)
+        else:
+            self.engine = registry.get(src.family).engine(src.params, bs[-1], dev, buckets=bs)
+        tp = tuning_path(src.family, bs[-1])
         if tp.exists():
             self.engine.load_tuning(tp)
         dt = torch.uint8 if in_kind == "u8" else torch.float32
-        self.staging = torch.zeros((bs[-1], IMG, IMG, 3), dtype=dt).pin_memory()
-        self.out = torch.zeros((bs[-1], self.engine.head.classes), dtype=torch.float32).pin_memory()
+        S = src.input_size
+        self.staging = torch.zeros((bs[-1], S, S, 3), dtype=dt).pin_memory()
+        self.out = torch.zeros((bs[-1], src.classes), dtype=torch.float32).pin_memory()
         for bk in bs:                         # warm-up + capture one hipGraph per bucket
             self.engine.program(bk, capture=True)
             self.engine.launch(bk)
@@ -193,18 +226,27 @@ class CPUExecutor(_Executor):
 
     def setup(self):
         bs = self.runner.buckets[-1]
+        src = self.runner.source
         u8 = self.runner.sig.input_dtype == P.DT_UINT8
-        self.staging = torch.zeros((bs, IMG, IMG, 3), dtype=torch.uint8 if u8 else torch.float32)
-        self.out = torch.zeros((bs, self.runner.source.head.classes), dtype=torch.float32)
+        S = src.input_size
+        self.staging = torch.zeros((bs, S, S, 3), dtype=torch.uint8 if u8 else torch.float32)
+        self.out = torch.zeros((bs, src.classes), dtype=torch.float32)
         self.u8 = u8
+        if src.family != "xception":
+            from ..engine import registry
+            self.oracle = registry.get(src.family).oracle
 
     def staging_ptr(self) -> int:
         return self.staging.data_ptr()
 
     def execute(self, bucket: int, n_real: int) -> int:
         x = self.staging[:n_real]
+        src = self.runner.source
+        if src.family != "xception":
+            self.out[:n_real] = self.oracle(src.params, x)
+            return self.out.data_ptr()
         x = x.float() / 127.5 - 1.0 if self.u8 else x
-        self.out[:n_real] = X.xception_forward(self.runner.source.params, x, head=self.runner.source.head)
+        self.out[:n_real] = X.xception_forward(src.params, x, head=src.head)
         return self.out.data_ptr()
 
 
@@ -216,12 +258,13 @@ class SignatureRunner:
         bp = cfg.batching
         self.buckets = sorted(set(bp.allowed_batch_sizes)) if cfg.enable_batching else [bp.max_batch_size]
         self.max_batch = self.buckets[-1]
-        item_bytes = IMG * IMG * 3 * (1 if sig.input_dtype == P.DT_UINT8 else 4)
+        S = source.input_size
+        item_bytes = S * S * 3 * (1 if sig.input_dtype == P.DT_UINT8 else 4)
         timeout = bp.batch_timeout_micros if cfg.enable_batching else 0
         self.batcher = _lib.rt().DynamicBatcher(max_batch_size=self.max_batch, batch_timeout_us=timeout,
                                                 max_enqueued_batches=bp.max_enqueued_batches,
                                                 allowed_batch_sizes=self.buckets, item_bytes=item_bytes,
-                                                out_cols=source.head.classes)
+                                                out_cols=source.classes)
         self.executors: list[_Executor] = []
         if devices:
             for d in devices:
@@ -240,9 +283,10 @@ class SignatureRunner:
     def predict(self, payload, n: int, deadline_us: int) -> np.ndarray:
         """payload: buffer of n items (uint8 or f32 images); returns f32 [n, classes]."""
         rt = _lib.rt()
-        ncls = self.source.head.classes
+        ncls = self.source.classes
         out = np.empty((n, ncls), dtype=np.float32)
-        item_bytes = IMG * IMG * 3 * (1 if self.sig.input_dtype == P.DT_UINT8 else 4)
+        S = self.source.input_size
+        item_bytes = S * S * 3 * (1 if self.sig.input_dtype == P.DT_UINT8 else 4)
         mv = memoryview(payload).cast("B")
         tickets = []
         for s in range(0, n, self.max_batch):

@@ -18,7 +18,7 @@ import numpy as np
 
 from ..ops import _lib
 from . import protos as P
-from .backend import IMG, ServingError
+from .backend import ServingError
 from .metrics import METRICS
 from .model_repo import ModelManager
 
@@ -42,6 +42,7 @@ def _abort(context, err: ServingError):
 def _payload(raw: bytes, td: dict, sig) -> tuple[object, int]:
     """Return (buffer of n images in the signature's dtype, n) from a parsed input."""
     dims = list(td["dims"])
+    IMG = sig.input_shape[1]
     if td["dtype"] != sig.input_dtype:
         raise ServingError("INVALID_ARGUMENT",
                            f"Expects arg[0] to be {P.DTYPE_NAMES.get(sig.input_dtype)} but "

@@ -101,8 +101,9 @@ def make_handler(manager: ModelManager):
                     x, rows = np.asarray(inp, dtype=dt), False
                 else:
                     raise ServingError("INVALID_ARGUMENT", "request must contain 'instances' or 'inputs'")
-                if x.ndim != 4 or x.shape[1:] != (299, 299, 3):
-                    raise ServingError("INVALID_ARGUMENT", f"expected images [-1,299,299,3], got {list(x.shape)}")
+                S = sig.input_shape[1]
+                if x.ndim != 4 or x.shape[1:] != (S, S, 3):
+                    raise ServingError("INVALID_ARGUMENT", f"expected images [-1,{S},{S},3], got {list(x.shape)}")
                 x = np.ascontiguousarray(x)
                 dl = self.headers.get("X-Deadline-Ms")
                 deadline = int(_lib.rt().now_us() + float(dl) * 1e3) if dl else 0

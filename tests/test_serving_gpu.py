@@ -67,3 +67,26 @@ def test_rccl_world1_dp_runner():
         assert not stopped and logits[:, 0].tolist() == [0.0, 1.0, 2.0]
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("family", ["resnet50", "vit_b16"])
+def test_gpu_serving_other_families(tmp_path, family):
+    from kdl.engine import registry
+    info = registry.get(family)
+    base = tmp_path / family
+    (base / "1").mkdir(parents=True)
+    (base / "1" / "synthetic.json").write_text('{"seed": 2, "model": "%s"}' % family)
+    cfg = ServerConfig(port=0, rest_api_port=0, model_name=family, model_base_path=str(base), device="gpu", gpus=1,
+                       host="127.0.0.1", file_system_poll_wait_seconds=0,
+                       batching=BatchingParams(max_batch_size=4, batch_timeout_micros=1000, allowed_batch_sizes=[2, 4]))
+    srv = ModelServer(cfg).start(block_until_loaded=True)
+    try:
+        S = info.input_size
+        x = np.random.default_rng(1).integers(0, 256, (3, S, S, 3), dtype=np.uint8)
+        stub = PredictionStub(grpc.insecure_channel(f"127.0.0.1:{srv.grpc_port}"))
+        r = stub.Predict(make_request(x, model_name=family, input_key="images"), timeout=120)
+        got = torch.from_numpy(np.asarray(r.outputs["logits"].float_val, np.float32).reshape(3, info.classes))
+        ref = info.oracle(info.init_params(2), torch.from_numpy(x))
+        assert torch.nn.functional.cosine_similarity(got, ref, dim=1).min() > 0.98
+    finally:
+        srv.stop(0)
