@@ -20,16 +20,30 @@ __device__ __forceinline__ long out_offset(const ConvGemmArgs& a, int m) {
   return (((long)b * (a.OH + 2) + oh + 1) * (a.OW + 2) + ow + 1) * a.ldy;
 }
 
-// pre-residual activation of the fp32 accumulator + bias (relu_out 1 ReLU, 3 exact GELU, 4 SiLU)
-__device__ __forceinline__ float act_pre(int mode, float v) {
-  if (mode == 1) return fmaxf(v, 0.f);
-  if (mode == 3) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-  if (mode == 4) return v / (1.f + __expf(-v));
+// Transcendental activations (relu_out 3 exact GELU, 4 SiLU) run here, in the
+// store pass over the bf16 C tile (8 values per call, one copy of the code),
+// NOT on the MFMA accumulators: expanding erff/expf over every accumulator
+// element of every fragment grew the GEMM from ~700 to ~4000 instructions and
+// cost 15-30 % on GEMMs that never use them. ReLU (1) stays on the accumulators.
+__device__ __noinline__ u32x4 act_transcendental(int mode, u32x4 v) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    float lo = bf_lo(v[d]), hi = bf_hi(v[d]);
+    if (mode == 3) {
+      lo = 0.5f * lo * (1.f + erff(lo * 0.70710678118654752f));
+      hi = 0.5f * hi * (1.f + erff(hi * 0.70710678118654752f));
+    } else {
+      lo = lo / (1.f + __expf(-lo));
+      hi = hi / (1.f + __expf(-hi));
+    }
+    v[d] = pack_bf16(lo, hi);
+  }
   return v;
 }
 
-// v: 8 bf16 (bias + optional pre-residual activation already applied) for row m, cols n..n+7
+// v: 8 bf16 (bias + optional pre-residual ReLU already applied) for row m, cols n..n+7
 __device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u32x4 v) {
+  if (a.relu_out >= 3) v = act_transcendental(a.relu_out, v);
   if (a.res) {
     const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
 #pragma unroll

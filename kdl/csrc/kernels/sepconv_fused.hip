@@ -207,9 +207,8 @@ __global__ __launch_bounds__(64 * NW) void sepconv_fused_kernel(ConvGemmArgs a, 
       const int ml = i * 16 + col;
       float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y;
       float v2 = acc[i][j][2] + bv.z, v3 = acc[i][j][3] + bv.w;
-      if (a.relu_out == 1 || a.relu_out >= 3) {
-        v0 = act_pre(a.relu_out, v0); v1 = act_pre(a.relu_out, v1);
-        v2 = act_pre(a.relu_out, v2); v3 = act_pre(a.relu_out, v3);
+      if (a.relu_out == 1) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       }
       *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
     }

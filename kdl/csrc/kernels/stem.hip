@@ -16,13 +16,15 @@
 
 namespace kdl {
 
-template <int IN_KIND, int NF>
+// GENERIC=false: 'valid' conv with the normalisation folded into the weights (the
+// Xception stem): no bounds checks, no per-element scale/shift.
+template <int IN_KIND, int NF, int KW, bool GENERIC>
 __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int M = a.B * a.OH * a.OW;
   const int OHW = a.OH * a.OW;
   const int m_wave = blockIdx.x * 128 + wave * 32;
-  const int KK = a.KH * a.KW * 3;
+  const int KK = a.KH * KW * 3;
   const int KT = (KK + 31) >> 5;
 
   long pbase[2];
@@ -51,8 +53,8 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
       const int k = ks * 32 + kq + j;
       const int tap = k / 3;
       ch[j] = k < KK ? k - 3 * tap : -1;
-      dy[j] = tap / a.KW;
-      dx[j] = tap - dy[j] * a.KW;
+      dy[j] = tap / KW;                  // compile-time divisor
+      dx[j] = tap - dy[j] * KW;
     }
     s16x8 bw[NF];
 #pragma unroll
@@ -64,14 +66,18 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
       for (int j = 0; j < 8; ++j) {
         const int ih = ih0[f] + dy[j], iw = iw0[f] + dx[j];
         float v = 0.f;
-        if (ch[j] >= 0 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
+        if (ch[j] >= 0 && (!GENERIC || ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W))) {
           const long p = (pbase[f] + (long)ih * a.W + iw) * 3 + ch[j];
           float raw;
           if constexpr (IN_KIND == 0) raw = (float)((const uint8_t*)a.x)[p];
           else raw = ((const float*)a.x)[p];
-          const int c = ch[j];
-          v = raw * (c == 0 ? a.scale[0] : c == 1 ? a.scale[1] : a.scale[2]) +
-              (c == 0 ? a.shift[0] : c == 1 ? a.shift[1] : a.shift[2]);
+          if constexpr (GENERIC) {
+            const int c = ch[j];
+            v = raw * (c == 0 ? a.scale[0] : c == 1 ? a.scale[1] : a.scale[2]) +
+                (c == 0 ? a.shift[0] : c == 1 ? a.shift[1] : a.shift[2]);
+          } else {
+            v = raw;
+          }
         }
         af[j] = (short)f2bf(v);
       }
@@ -102,13 +108,15 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
   }
 }
 
-template <int IN_KIND>
+template <int IN_KIND, int KW>
 static hipError_t launch_stem(const StemArgs& a, dim3 grid, hipStream_t s) {
-  switch (a.cout) {
-    case 32: hipLaunchKernelGGL((stem_kernel<IN_KIND, 2>), grid, dim3(256), 0, s, a); break;
-    case 64: hipLaunchKernelGGL((stem_kernel<IN_KIND, 4>), grid, dim3(256), 0, s, a); break;
-    default: return hipErrorInvalidValue;
-  }
+  const bool generic = a.pad != 0 || a.scale[0] != 1.f || a.scale[1] != 1.f || a.scale[2] != 1.f ||
+                       a.shift[0] != 0.f || a.shift[1] != 0.f || a.shift[2] != 0.f;
+  if (a.cout == 32 && !generic) hipLaunchKernelGGL((stem_kernel<IN_KIND, 2, KW, false>), grid, dim3(256), 0, s, a);
+  else if (a.cout == 32) hipLaunchKernelGGL((stem_kernel<IN_KIND, 2, KW, true>), grid, dim3(256), 0, s, a);
+  else if (a.cout == 64 && !generic) hipLaunchKernelGGL((stem_kernel<IN_KIND, 4, KW, false>), grid, dim3(256), 0, s, a);
+  else if (a.cout == 64) hipLaunchKernelGGL((stem_kernel<IN_KIND, 4, KW, true>), grid, dim3(256), 0, s, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -116,8 +124,10 @@ hipError_t stem_conv(const StemArgs& a, hipStream_t s) {
   const int M = a.B * a.OH * a.OW;
   if (M <= 0 || a.ldy < a.cout || a.KH <= 0 || a.KW <= 0 || a.stride <= 0) return hipErrorInvalidValue;
   const dim3 grid((M + 127) / 128);
-  if (a.in_kind == 0) return launch_stem<0>(a, grid, s);
-  if (a.in_kind == 1) return launch_stem<1>(a, grid, s);
+  if (a.KW == 3 && a.in_kind == 0) return launch_stem<0, 3>(a, grid, s);
+  if (a.KW == 3 && a.in_kind == 1) return launch_stem<1, 3>(a, grid, s);
+  if (a.KW == 7 && a.in_kind == 0) return launch_stem<0, 7>(a, grid, s);
+  if (a.KW == 7 && a.in_kind == 1) return launch_stem<1, 7>(a, grid, s);
   return hipErrorInvalidValue;
 }
 
