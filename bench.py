@@ -6,11 +6,12 @@ One process per GPU (``torch.distributed.run``), RCCL over xGMI. A timed step is
 one dynamic batch of 32 images per GPU (weak scaling, global batch 32*N):
 
   1. ingress: rank 0 copies the uint8 batch [32N,299,299,3] host(pinned)->device
-     on a copy stream, double-buffered (batch i+1's H2D overlaps batch i);
+     on a copy stream;
   2. scatter: RCCL scatter of uint8 shards (4x fewer bytes than f32)
-     straight into every rank's static engine input buffer;
-  3. forward: one hipGraph replay of the fused HIP-kernel Xception (41 launches);
-  4. gather:  RCCL gather of the fp32 logits to rank 0, D2H to host.
+     on a comm stream, straight into one of every rank's two engine input slots;
+  3. forward: one hipGraph replay of the fused HIP-kernel model on the compute stream;
+  4. gather:  RCCL gather of the fp32 logits to rank 0 (comm stream), D2H (egress stream).
+Steps are software-pipelined: batch i+1's H2D + scatter overlap batch i's forward.
 
 ``--ingress local`` instead has every rank H2D its own shard (host-direct mode,
 no rank-0 bottleneck). Data is synthetic (random uint8 images) and the weights are
@@ -45,6 +46,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--profile-layers", action="store_true")
     ap.add_argument("--save-tuning", default=None, help="write the autotune result (rank 0) to this path")
+    ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # gloo: pipeline logic checks
     a = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -52,11 +54,15 @@ def main(argv=None) -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(a.dist_backend)
 
     from kdl.engine import registry
     from kdl.engine.tuning import tuning_path
@@ -91,52 +97,73 @@ def main(argv=None) -> int:
     stage = ([torch.empty((n_host, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(2)]
              if has_host and not direct else [None, None])
     NC = info.classes
-    # logits are double-buffered too and leave through their own D2H stream, so the
-    # small D2H never queues the next batch's graph behind the ingress DMA
-    logits_all = [torch.empty((n_global, NC), dtype=torch.float32, device=dev) for _ in range(2)]
-    out_host = [torch.empty((n_global, NC), dtype=torch.float32).pin_memory() for _ in range(2)]
-    s = eng.stream
-    cs = torch.cuda.Stream(device=dev)
-    ds = torch.cuda.Stream(device=dev)
-    ready = [torch.cuda.Event() for _ in range(2)]
-    free = [torch.cuda.Event() for _ in range(2)]
-    done = [torch.cuda.Event() for _ in range(2)]
-    drained = [torch.cuda.Event() for _ in range(2)]
-    for e in free + drained:
+    # per-slot device copy of the logits (the next graph overwrites eng.logits), the
+    # gathered logits and their pinned host copies; all double-buffered
+    lbuf = [torch.zeros((B, NC), dtype=torch.float32, device=dev) for _ in range(2)]
+    logits_all = [torch.zeros((n_global, NC), dtype=torch.float32, device=dev) for _ in range(2)]
+    out_host = [torch.zeros((n_global, NC), dtype=torch.float32).pin_memory() for _ in range(2)]
+    s = eng.stream                          # compute: graph replays
+    cs = torch.cuda.Stream(device=dev)      # ingress H2D
+    ms = torch.cuda.Stream(device=dev)      # RCCL scatter / gather (overlaps the compute stream)
+    ds = torch.cuda.Stream(device=dev)      # egress D2H
+    E = lambda: [torch.cuda.Event() for _ in range(2)]  # noqa: E731
+    ready, scattered, free, done, gathered, drained = E(), E(), E(), E(), E(), E()
+    for e in free + gathered + drained + scattered:
         e.record(s)
     total = a.warmup + a.steps
-    t_in = [torch.cuda.Event(enable_timing=True) for _ in range(total)]
-    t_out = [torch.cuda.Event(enable_timing=True) for _ in range(total)]
+    t_in = [torch.cuda.Event(enable_timing=True) for _ in range(total + 1)]
+    t_out = [torch.cuda.Event(enable_timing=True) for _ in range(total + 1)]
 
-    def step(i, timed=False):
+    # Software pipeline, one batch per step: while the graph of batch i runs on the
+    # compute stream, batch i+1 is H2D'd (copy stream) and RCCL-scattered (comm stream).
+    def ingress(i, timed=False):
         j = i % 2
         with torch.cuda.stream(cs):
-            cs.wait_event(free[j])
+            cs.wait_event(free[j])          # slot j no longer read by the graph of batch i-2
+            cs.wait_event(scattered[j])     # stage j no longer read by the scatter of batch i-2
             if timed:
                 t_in[i].record(cs)
             if has_host:
                 (slots[j][:B] if direct else stage[j]).copy_(host, non_blocking=True)
             ready[j].record(cs)
-        with torch.cuda.stream(s):
-            s.wait_event(ready[j])
-            if not direct:
+        if not direct:
+            with torch.cuda.stream(ms):
+                ms.wait_event(ready[j])
                 dist.scatter(slots[j][:B], list(stage[j].chunk(world)) if rank == 0 else None, src=0)
+                scattered[j].record(ms)
+
+    def compute(i):
+        j = i % 2
+        with torch.cuda.stream(s):
+            s.wait_event(ready[j] if direct else scattered[j])
             eng.launch(B, s, capture=use_graph, slot=j)
             free[j].record(s)
-            s.wait_event(drained[j])
-            logits = eng.logits[:B]
-            if world > 1:
-                dist.gather(logits, list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
-            else:
-                logits_all[j].copy_(logits)
+            s.wait_event(gathered[j])       # lbuf j no longer read by the gather of batch i-2
+            lbuf[j].copy_(eng.logits[:B])
             done[j].record(s)
+
+    def collect(i, timed=False):
+        j = i % 2
+        with torch.cuda.stream(ms):
+            ms.wait_event(done[j])
+            ms.wait_event(drained[j])       # logits_all j no longer read by the D2H of batch i-2
+            if world > 1:
+                dist.gather(lbuf[j], list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
+            else:
+                logits_all[j].copy_(lbuf[j])
+            gathered[j].record(ms)
         with torch.cuda.stream(ds):
-            ds.wait_event(done[j])
+            ds.wait_event(gathered[j])
             if rank == 0:
                 out_host[j].copy_(logits_all[j], non_blocking=True)
             drained[j].record(ds)
             if timed:
                 t_out[i].record(ds)
+
+    def step(i):
+        ingress(i + 1)        # prefetch the next batch (K timed steps = K ingresses + K forwards)
+        compute(i)
+        collect(i)
 
     # setup (not a warmup step): capture both slots' graphs and let the clocks ramp
     for j in range(2):
@@ -148,6 +175,7 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    ingress(0)
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -173,7 +201,9 @@ def main(argv=None) -> int:
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        step(k, timed=True)
+        ingress(k, timed=True)
+        compute(k)
+        collect(k, timed=True)
         torch.cuda.synchronize()
         lat.append(t_in[k].elapsed_time(t_out[k]))
     if world > 1:
@@ -182,7 +212,7 @@ def main(argv=None) -> int:
         lat = t.tolist()
 
     if rank == 0:
-        ms = elapsed * 1e3 / a.steps
+        ms_step = elapsed * 1e3 / a.steps
         img_s = n_global * a.steps / elapsed
         res = {
             "metric": ("images/sec (whole node) + p50 latency, Xception 299x299 at 1/2/4/8 MI355X"
@@ -193,7 +223,7 @@ def main(argv=None) -> int:
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(ms, 4),
+            "ms_per_step": round(ms_step, 4),
             "p50_latency_ms": round(statistics.median(lat), 4),
             "p99_latency_ms": round(sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))], 4),
             "settle_s": a.settle,
