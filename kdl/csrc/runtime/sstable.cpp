@@ -93,6 +93,9 @@ std::string snappy_uncompress(const uint8_t* data, size_t n) {
   const uint8_t* p = data;
   const uint8_t* end = data + n;
   const uint64_t len = get_varint(p, end);
+  // untrusted header: a snappy element expands at most 64x (a 3-byte copy of 64
+  // bytes), so a larger claim is corrupt -- and must not reach reserve()
+  if (len > uint64_t(n) * 64 + 64) throw std::runtime_error("snappy: implausible uncompressed length");
   std::string out;
   out.reserve(len);
   while (p < end) {
@@ -109,6 +112,7 @@ std::string snappy_uncompress(const uint8_t* data, size_t n) {
       }
       l += 1;
       if (uint64_t(end - p) < l) throw std::runtime_error("snappy: truncated literal");
+      if (out.size() + l > len) throw std::runtime_error("snappy: output overrun");
       out.append(reinterpret_cast<const char*>(p), l);
       p += l;
     } else {
@@ -129,6 +133,7 @@ std::string snappy_uncompress(const uint8_t* data, size_t n) {
         p += 4;
       }
       if (off == 0 || off > out.size()) throw std::runtime_error("snappy: bad offset");
+      if (out.size() + l > len) throw std::runtime_error("snappy: output overrun");
       const size_t from = out.size() - off;
       for (uint64_t i = 0; i < l; ++i) out.push_back(out[from + i]);  // may overlap
     }
