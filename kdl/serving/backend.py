@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -132,9 +133,50 @@ def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
     return ModelSource(params=params, head=head, signatures=sigs, origin=origin, classes=head.classes)
 
 
+# ---------------------------------------------------------------------- fault injection
+class FaultInjector:
+    """Test hook (SURVEY.md §5 "fault-injection hooks (env/flag) to fail a device or
+    delay a batch"): ``KDL_FAULT_INJECT="fail=gpu1:-1,delay=cpu:50"`` makes every
+    executor whose name contains ``gpu1`` raise on its batches (count -1 = forever,
+    n = the next n batches) and delays batches of executors matching ``cpu`` by 50 ms."""
+
+    def __init__(self, spec: str | None = None):
+        spec = os.environ.get("KDL_FAULT_INJECT", "") if spec is None else spec
+        self.fail: dict[str, int] = {}
+        self.delay: dict[str, float] = {}
+        self._lock = threading.Lock()
+        for rule in filter(None, (r.strip() for r in spec.split(","))):
+            kind, _, rest = rule.partition("=")
+            pat, _, val = rest.partition(":")
+            if kind == "fail":
+                self.fail[pat] = int(val or -1)
+            elif kind == "delay":
+                self.delay[pat] = float(val or 0) / 1e3
+            else:
+                raise ValueError(f"bad KDL_FAULT_INJECT rule {rule!r}")
+
+    def before_batch(self, executor: str) -> None:
+        for pat, sec in self.delay.items():
+            if pat in executor:
+                time.sleep(sec)
+        with self._lock:
+            for pat, left in self.fail.items():
+                if pat in executor and left != 0:
+                    if left > 0:
+                        self.fail[pat] = left - 1
+                    raise RuntimeError(f"injected fault on {executor}")
+
+
 # ---------------------------------------------------------------------- executors
 class _Executor(threading.Thread):
-    """Pulls batches from a DynamicBatcher and runs them on one device."""
+    """Pulls batches from a DynamicBatcher and runs them on one device.
+
+    Per-device fault isolation: after ``max_failures`` consecutive failed batches
+    the executor marks its device unhealthy and stops pulling, so the shared
+    batcher routes everything to the remaining devices; the servable reports not
+    ready once no healthy executor is left."""
+
+    max_failures = 3
 
     def __init__(self, runner: "SignatureRunner", name: str):
         super().__init__(name=name, daemon=True)
@@ -142,6 +184,9 @@ class _Executor(threading.Thread):
         self.stop = threading.Event()
         self.ready = threading.Event()
         self.error: BaseException | None = None
+        self.healthy = True
+        self.failures = 0
+        self.faults = runner.faults
 
     def run(self):
         try:
@@ -152,6 +197,7 @@ class _Executor(threading.Thread):
             self.ready.set()
             return
         self.ready.set()
+        METRICS.gauge("kdl_executor_healthy", lambda: float(self.healthy), executor=self.name)
         b = self.runner.batcher
         rt = _lib.rt()
         while not self.stop.is_set():
@@ -160,12 +206,20 @@ class _Executor(threading.Thread):
                 continue
             t0 = time.perf_counter()
             try:
+                self.faults.before_batch(self.name)
                 out_ptr = self.execute(batch.bucket, batch.n_real)
                 b.finish(batch, out_ptr, rt.ST_OK)
+                self.failures = 0
             except BaseException:  # noqa: BLE001 - fail the batch, keep serving
                 log.exception("batch %d failed on %s", batch.id, self.name)
                 b.finish(batch, 0, rt.ST_ERROR)
                 METRICS.inc("kdl_batch_errors_total", executor=self.name)
+                self.failures += 1
+                if self.failures >= self.max_failures:
+                    self.healthy = False
+                    log.error("executor %s: %d consecutive failures, marking device unhealthy and leaving "
+                              "the batcher to the other devices", self.name, self.failures)
+                    return
                 continue
             dt = (time.perf_counter() - t0) * 1e3
             METRICS.observe("kdl_batch_exec_ms", dt, executor=self.name)
@@ -221,8 +275,8 @@ class GPUExecutor(_Executor):
 
 
 class CPUExecutor(_Executor):
-    def __init__(self, runner):
-        super().__init__(runner, f"cpu/{runner.sig.name}")
+    def __init__(self, runner, index: int = 0):
+        super().__init__(runner, f"cpu{index}/{runner.sig.name}")
 
     def setup(self):
         bs = self.runner.buckets[-1]
@@ -266,12 +320,14 @@ class SignatureRunner:
                                                 allowed_batch_sizes=self.buckets, item_bytes=item_bytes,
                                                 out_cols=source.classes)
         self.executors: list[_Executor] = []
+        self.faults = FaultInjector()
         if devices:
             for d in devices:
                 for _ in range(max(1, cfg.executors_per_gpu)):
                     self.executors.append(GPUExecutor(self, d, {}))
         else:
-            self.executors.append(CPUExecutor(self))
+            for i in range(max(1, cfg.executors_per_gpu)):
+                self.executors.append(CPUExecutor(self, i))
         for ex in self.executors:
             ex.start()
         for ex in self.executors:
@@ -283,6 +339,8 @@ class SignatureRunner:
     def predict(self, payload, n: int, deadline_us: int) -> np.ndarray:
         """payload: buffer of n items (uint8 or f32 images); returns f32 [n, classes]."""
         rt = _lib.rt()
+        if not self.healthy():
+            raise ServingError("UNAVAILABLE", f"no healthy device left for signature {self.sig.name}")
         ncls = self.source.classes
         out = np.empty((n, ncls), dtype=np.float32)
         S = self.source.input_size
@@ -314,6 +372,9 @@ class SignatureRunner:
             raise ServingError("INTERNAL" if status == rt.ST_ERROR else "UNAVAILABLE", f"batch failed (status {status})")
         return out
 
+    def healthy(self) -> bool:
+        return any(ex.healthy and ex.error is None for ex in self.executors)
+
     def close(self):
         for ex in self.executors:
             ex.stop.set()
@@ -344,6 +405,10 @@ class Servable:
                 r = self.runners[sig_name] = SignatureRunner(self.signatures[sig_name], self.source,
                                                              self._cfg, self._devices)
             return r
+
+    def healthy(self) -> bool:
+        with self._lock:
+            return all(r.healthy() for r in self.runners.values())
 
     def close(self):
         for r in self.runners.values():

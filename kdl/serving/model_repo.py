@@ -125,8 +125,10 @@ class ModelManager:
             return self.servables[max(self.servables)]
 
     def ready(self) -> bool:
+        """A version is loaded (graphs captured) and it still has a healthy device."""
         with self._lock:
-            return bool(self.servables)
+            servables = list(self.servables.values())
+        return bool(servables) and all(s.healthy() for s in servables)
 
     def status(self, version: int | None = None) -> list[tuple[int, int, str]]:
         with self._lock:
