@@ -205,6 +205,7 @@ class _Executor(threading.Thread):
             if batch is None:
                 continue
             t0 = time.perf_counter()
+            METRICS.observe("kdl_stage_ms", (rt.now_us() - batch.oldest_enqueue_us) / 1e3, stage="queue_wait")
             try:
                 self.faults.before_batch(self.name)
                 out_ptr = self.execute(batch.bucket, batch.n_real)

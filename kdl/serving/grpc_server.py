@@ -100,8 +100,14 @@ class Servicer:
                 if f != sig.output_key:
                     raise ServingError("INVALID_ARGUMENT", f"output tensor alias not found in signature: {f}")
             buf, n = _payload(raw, inputs[sig.input_key], sig)
+            t1 = time.perf_counter()
             logits = runner.predict(buf, n, _deadline_us(context))
+            t2 = time.perf_counter()
             out = rt.build_predict_response([(sig.output_key, logits)], s.name, s.version, sig_name)
+            # per-request stage trace (SURVEY.md §5 tracing): parse+validate, batcher wait+run, respond
+            METRICS.observe("kdl_stage_ms", (t1 - t0) * 1e3, stage="parse")
+            METRICS.observe("kdl_stage_ms", (t2 - t1) * 1e3, stage="batch_and_run")
+            METRICS.observe("kdl_stage_ms", (time.perf_counter() - t2) * 1e3, stage="respond")
         except ServingError as e:
             METRICS.inc("kdl_requests_total", code=e.code, method="Predict")
             _abort(context, e)

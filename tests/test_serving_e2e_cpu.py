@@ -151,6 +151,8 @@ def test_rest_api(server):
     assert len(out["predictions"]) == 1 and len(out["predictions"][0]) == 10
     text = urllib.request.urlopen(f"{base}/monitoring/prometheus/metrics").read().decode()
     assert "kdl_requests_total" in text
+    for stage in ("parse", "queue_wait", "batch_and_run", "respond"):   # per-request stage trace
+        assert f'stage="{stage}"' in text, stage
     assert urllib.request.urlopen(f"{base}/readyz").status == 200
 
 
