@@ -40,7 +40,8 @@ def main(argv=None) -> int:
     ap.add_argument("--settle", type=float, default=0.5,
                     help="seconds of untimed graph replays before the warmup steps (GPU clock ramp)")
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
-    ap.add_argument("--model", default="xception", help="xception (headline) | resnet50")
+    ap.add_argument("--model", default="xception",
+                    help="xception (headline) | resnet50 | vit_b16 | vit_b16_fp8 | efficientnet_b7")
     ap.add_argument("--ingress", choices=["scatter", "local"], default="scatter")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-tune", action="store_true")
@@ -233,7 +234,7 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": (None if BASELINE_IMG_S is None or a.model != "xception"
                             else round(img_s / BASELINE_IMG_S, 3)),
-            "dtype": "bf16",
+            "dtype": "fp8-e4m3 linears / bf16 rest" if a.model.endswith("_fp8") else "bf16",
             "data": f"synthetic uint8 {S}x{S}x3 images, random-init weights",
             "config": {"model": info.description,
                        "global_batch": n_global, "seq_len": None, "image_size": S,

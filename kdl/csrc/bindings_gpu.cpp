@@ -90,6 +90,7 @@ LnArgs ln_args(const py::dict& d) {
   LnArgs a{};
   a.x = P<const uint16_t>(d, "x"); a.y = P<uint16_t>(d, "y");
   a.gamma = P<const float>(d, "gamma"); a.beta = P<const float>(d, "beta");
+  a.y8 = P<uint8_t>(d, "y8"); a.inv_scale = F(d, "inv_scale", 1.f);
   a.rows = d["rows"].cast<long>(); a.D = I(d, "D"); a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy");
   a.eps = F(d, "eps", 1e-6f);
   return a;
@@ -97,6 +98,7 @@ LnArgs ln_args(const py::dict& d) {
 AttnArgs attn_args(const py::dict& d) {
   AttnArgs a{};
   a.qkv = P<const uint16_t>(d, "qkv"); a.out = P<uint16_t>(d, "out");
+  a.out8 = P<uint8_t>(d, "out8"); a.inv_scale = F(d, "inv_scale", 1.f);
   a.B = I(d, "B"); a.T = I(d, "T"); a.H = I(d, "H"); a.dh = I(d, "dh", 64);
   a.scale = F(d, "scale", 0.125f);
   return a;
@@ -120,6 +122,15 @@ ChScaleArgs chs_args(const py::dict& d) {
   ChScaleArgs a{};
   a.y = P<uint16_t>(d, "y"); a.scale = P<const float>(d, "scale");
   a.B = I(d, "B"); a.HW = I(d, "HW"); a.C = I(d, "C");
+  return a;
+}
+GemmF8Args f8_args(const py::dict& d) {
+  GemmF8Args a{};
+  a.x = P<const uint8_t>(d, "x"); a.wp = P<const uint8_t>(d, "wp"); a.bias = P<const float>(d, "bias");
+  a.colscale = P<const float>(d, "colscale"); a.res = P<const uint16_t>(d, "res");
+  a.y = P<uint16_t>(d, "y"); a.y8 = P<uint8_t>(d, "y8"); a.out_inv_scale = F(d, "out_inv_scale", 1.f);
+  a.M = I(d, "M"); a.K = I(d, "K"); a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
+  a.NF = I(d, "NF"); a.nstore = I(d, "nstore"); a.relu_out = I(d, "relu_out");
   return a;
 }
 FcMfmaArgs fcm_args(const py::dict& d) {
@@ -250,6 +261,20 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(channel_scale(a, S(s)), "channel_scale");
   });
+  m.def("gemm_f8", [](int cfg, py::dict d, uintptr_t s) {
+    const auto a = f8_args(d);
+    py::gil_scoped_release nogil;
+    chk(gemm_f8(cfg, a, S(s)), "gemm_f8");
+  });
+  m.def("gemm_f8_config", [](int cfg) {
+    int bm = 0, bn = 0, th = 0;
+    if (gemm_f8_config(cfg, &bm, &bn, &th) != 0) throw std::out_of_range("bad gemm_f8 config");
+    return py::make_tuple(bm, bn, th);
+  });
+  m.def("mfma_f8_probe", [](uintptr_t a, uintptr_t b, uintptr_t d, uintptr_t s) {
+    chk(mfma_f8_probe(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
+                      reinterpret_cast<float*>(d), S(s)), "mfma_f8_probe");
+  });
   m.def("fc_mfma", [](py::dict d, uintptr_t s) {
     const auto a = fcm_args(d);
     py::gil_scoped_release nogil;
@@ -307,6 +332,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_chscale", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_CHSCALE; op.name = name; op.cs = chs_args(d); p.add(op);
+      })
+      .def("add_gemm_f8", [](Program& p, const std::string& name, int cfg, py::dict d) {
+        Op op; op.kind = OP_GEMM_F8; op.name = name; op.cfg = cfg; op.f8 = f8_args(d); p.add(op);
       })
       .def("add_fc_mfma", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_FC_MFMA; op.name = name; op.fcm = fcm_args(d); p.add(op);

@@ -131,11 +131,19 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   l += __shfl_xor(l, 32);
   if (qvalid) {
     const float inv = 1.f / l;
-    uint16_t* op = a.out + ((long)b * a.T + qi) * (a.H * AT_DH) + h * AT_DH + 4 * q;
+    const long off = ((long)b * a.T + qi) * (a.H * AT_DH) + h * AT_DH + 4 * q;
+    if (a.out8) {
+      const float sc = inv * a.inv_scale;
 #pragma unroll
-    for (int df = 0; df < 4; ++df)
-      *(u32x2*)(op + 16 * df) = (u32x2){pack_bf16(o[df][0] * inv, o[df][1] * inv),
-                                        pack_bf16(o[df][2] * inv, o[df][3] * inv)};
+      for (int df = 0; df < 4; ++df)
+        *(uint32_t*)(a.out8 + off + 16 * df) = pack_fp8x4(o[df][0] * sc, o[df][1] * sc, o[df][2] * sc, o[df][3] * sc);
+    } else {
+      uint16_t* op = a.out + off;
+#pragma unroll
+      for (int df = 0; df < 4; ++df)
+        *(u32x2*)(op + 16 * df) = (u32x2){pack_bf16(o[df][0] * inv, o[df][1] * inv),
+                                          pack_bf16(o[df][2] * inv, o[df][3] * inv)};
+    }
   }
 }
 

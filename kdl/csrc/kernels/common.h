@@ -44,6 +44,15 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t d) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(v, z));
 }
 
+// 4 floats -> 4 OCP e4m3 bytes (saturated to +-448; gfx950 v_cvt_pk_fp8_f32 is OCP)
+__device__ __forceinline__ uint32_t pack_fp8x4(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f); b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f); d = fminf(fmaxf(d, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
 __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

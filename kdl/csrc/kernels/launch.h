@@ -136,6 +136,8 @@ hipError_t embed_tokens(const EmbedArgs& a, hipStream_t s);
 struct LnArgs {
   const uint16_t* x;
   uint16_t* y;
+  uint8_t* y8;            // optional e4m3 output (value * inv_scale) instead of y
+  float inv_scale;
   const float* gamma;
   const float* beta;
   long rows;
@@ -149,6 +151,8 @@ hipError_t layernorm(const LnArgs& a, hipStream_t s);
 struct AttnArgs {
   const uint16_t* qkv;
   uint16_t* out;
+  uint8_t* out8;          // optional e4m3 output (value * inv_scale) instead of out
+  float inv_scale;
   int B, T, H, dh;        // dh = 64
   float scale;            // 1/sqrt(dh)
 };
@@ -187,6 +191,24 @@ struct ChScaleArgs {
   int B, HW, C;
 };
 hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s);
+
+// FP8 (OCP e4m3) GEMM, gemm_f8.hip: y = act(colscale[n] * A8 W8^T + bias[n]) (+res), bf16 or fp8 out.
+struct GemmF8Args {
+  const uint8_t* x;       // A e4m3 [M][ldx bytes]
+  const uint8_t* wp;      // packed e4m3 [NF][K/128][2][64][16]
+  const float* bias;      // [NF*16]
+  const float* colscale;  // [NF*16] = s_a * s_w[n]
+  const uint16_t* res;    // optional bf16 residual [M][ldr]
+  uint16_t* y;            // bf16 out [M][ldy] (used when y8 is null)
+  uint8_t* y8;            // e4m3 out [M][ldy], value / out_scale
+  float out_inv_scale;
+  int M, K, ldx, ldy, ldr, NF, nstore, relu_out;
+};
+hipError_t gemm_f8(int cfg, const GemmF8Args& a, hipStream_t s);
+int gemm_f8_config(int cfg, int* bm, int* bn, int* threads);
+
+// Debug: one v_mfma_scale_f32_16x16x128_f8f6f4 on lane-ordered operands (64 x 32 B each).
+hipError_t mfma_f8_probe(const void* a, const void* b, float* d, hipStream_t s);
 
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {

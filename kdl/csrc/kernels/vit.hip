@@ -122,12 +122,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LnArgs a) {
       const float4 b0 = *(const float4*)(a.beta + c8 * 8), b1 = *(const float4*)(a.beta + c8 * 8 + 4);
       const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
       const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      u32x4 o;
+      float o8[8];
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
-        o[d] = pack_bf16((v[j][2 * d] - mean) * rstd * g[2 * d] + bb[2 * d],
-                         (v[j][2 * d + 1] - mean) * rstd * g[2 * d + 1] + bb[2 * d + 1]);
-      *(u32x4*)(yr + c8 * 8) = o;
+      for (int d = 0; d < 8; ++d) o8[d] = (v[j][d] - mean) * rstd * g[d] + bb[d];
+      if (a.y8) {
+        const float q = a.inv_scale;
+        *(u32x2*)(a.y8 + r * a.ldy + c8 * 8) = (u32x2){pack_fp8x4(o8[0] * q, o8[1] * q, o8[2] * q, o8[3] * q),
+                                                        pack_fp8x4(o8[4] * q, o8[5] * q, o8[6] * q, o8[7] * q)};
+      } else {
+        u32x4 o;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = pack_bf16(o8[2 * d], o8[2 * d + 1]);
+        *(u32x4*)(yr + c8 * 8) = o;
+      }
     }
   }
 }

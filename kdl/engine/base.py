@@ -71,7 +71,8 @@ class EngineBase:
 
     # ---------------------------------------------------------------- programs
     def conv_steps(self) -> list[Step]:
-        return [s for s in self.steps if s.kind == "conv"]
+        """Steps with a tunable GEMM layer (bf16 conv-GEMM or fp8 linear)."""
+        return [s for s in self.steps if s.kind in ("conv", "f8")]
 
     def program(self, b: int, capture: bool = True, slot: int = 0):
         key = (b, capture, slot)
@@ -175,6 +176,6 @@ class EngineBase:
             if v is None:
                 continue
             split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
-            if cfg in s.layer.candidates and (not split or s.layer.mode == MODE_DW):
+            if cfg in s.layer.candidates and (not split or getattr(s.layer, "mode", -1) == MODE_DW):
                 s.layer.split, s.layer.cfg = split, cfg
         self.invalidate()

@@ -62,7 +62,18 @@ def _efficientnet_b7():
                      E.efficientnet_forward)
 
 
-_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "vit_b16": _vit_b16,
+def _vit_b16_fp8():
+    from ..models import vit as V
+    from .vit import ViTEngine
+    return ModelInfo("vit_b16_fp8", V.INPUT_SIZE, 1000, V.TOTAL_PARAMS,
+                     "ViT-B/16 224x224, e4m3 linears (static per-tensor activation / per-channel weight scales)",
+                     lambda seed=0: V.init_params(seed=seed),
+                     lambda p, max_batch, device, **kw: ViTEngine(p, max_batch=max_batch, device=device, fp8=True,
+                                                                  **kw),
+                     V.vit_forward)
+
+
+_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "vit_b16": _vit_b16, "vit_b16_fp8": _vit_b16_fp8,
               "efficientnet_b7": _efficientnet_b7}
 
 

@@ -19,6 +19,12 @@ Lowering (captured into one hipGraph per batch bucket; rows = B*197 tokens):
 
 = 3 + 12*7 + 2 = 89 launches. Every linear layer runs on the same pipelined
 LDS-DMA MFMA GEMM as the CNNs (a 1x1 conv over a 1 x rows "image").
+
+fp8=True (BASELINE.json "fp8 MFMA" config): the four linears of every layer run on
+gemm_f8.hip (OCP e4m3 x e4m3, block-scaled MFMA 16x16x128); ln_1 / ln_2 /
+attention / the GELU GEMM write e4m3 directly with static per-tensor scales
+calibrated on the fp32 oracle (amax x 1.25 / 448); weights per output channel.
+The residual stream, QKV, softmax and the patch embedding / head stay bf16/fp32.
 """
 from __future__ import annotations
 
@@ -37,8 +43,17 @@ class ViTEngine(EngineBase):
     model_name = "vit_b16"
 
     def __init__(self, params: dict, max_batch: int = 32, device: str | torch.device = "cuda",
-                 buckets=None, tune_file: str | Path | None = None):
+                 buckets=None, tune_file: str | Path | None = None, fp8: bool = False,
+                 calib: torch.Tensor | None = None, calib_margin: float = 1.25):
         super().__init__(device, max_batch, buckets)
+        self.fp8 = fp8
+        if fp8:
+            self.model_name = "vit_b16_fp8"
+            if calib is None:   # synthetic calibration batch (serving would use real images)
+                calib = torch.randint(0, 256, (2, V.INPUT_SIZE, V.INPUT_SIZE, 3),
+                                      generator=torch.Generator().manual_seed(1234), dtype=torch.uint8)
+            self.amax = V.activation_amax(params, calib)
+            self.calib_margin = calib_margin
         self.size = V.INPUT_SIZE
         self.T = V.TOKENS
         self.np = self.T - 1
@@ -62,10 +77,14 @@ class ViTEngine(EngineBase):
         self.cls = p["class_token"].reshape(D).float().to(dev)
         self.pos = p["encoder.pos_embedding"].reshape(self.T, D).float().contiguous().to(dev)
         self.steps.append(Step("embed", "embed", dst="X"))
+        self.f8scale: dict[str, float] = {}
         for i in range(V.DEPTH):
             L = f"encoder.layers.encoder_layer_{i}"
             self.ln[f"{L}.ln_1"] = (p[f"{L}.ln_1.weight"].float().to(dev), p[f"{L}.ln_1.bias"].float().to(dev))
             self.ln[f"{L}.ln_2"] = (p[f"{L}.ln_2.weight"].float().to(dev), p[f"{L}.ln_2.bias"].float().to(dev))
+            if self.fp8:
+                self._build_layer_f8(p, i, L)
+                continue
             self.steps.append(Step("ln", f"{L}.ln_1", src="X", dst="Xn"))
             self.steps.append(Step("conv", f"{L}.qkv", self._lin(
                 f"{L}.qkv", p[f"{L}.self_attention.in_proj_weight"], p[f"{L}.self_attention.in_proj_bias"]),
@@ -87,6 +106,29 @@ class ViTEngine(EngineBase):
         self.head_b = p["heads.head.bias"].float().to(dev)
         self.steps.append(Step("fc", "heads.head", src="CLS", dst="logits"))
 
+    def _build_layer_f8(self, p: dict, i: int, L: str) -> None:
+        """One encoder layer with all four linears on the e4m3 GEMM (static scales)."""
+        from ..ops.f8 import E4M3_MAX, F8Linear
+        sc = {k: v * self.calib_margin / E4M3_MAX for k, v in self.amax[i].items()}
+        for k, v in sc.items():
+            self.f8scale[f"{L}.{k}"] = v
+        dev = self.device
+        self.steps.append(Step("ln", f"{L}.ln_1", src="X", dst="Xn8", extra=dict(out_scale=sc["ln_1"])))
+        self.steps.append(Step("f8", f"{L}.qkv", F8Linear(
+            f"{L}.qkv", p[f"{L}.self_attention.in_proj_weight"], p[f"{L}.self_attention.in_proj_bias"], sc["ln_1"],
+            device=dev), "Xn8", "QKV"))
+        self.steps.append(Step("attn", f"{L}.attn", src="QKV", dst="A8", extra=dict(out_scale=sc["attn"])))
+        self.steps.append(Step("f8", f"{L}.out_proj", F8Linear(
+            f"{L}.out_proj", p[f"{L}.self_attention.out_proj.weight"], p[f"{L}.self_attention.out_proj.bias"],
+            sc["attn"], device=dev), "A8", "X", res="X"))
+        self.steps.append(Step("ln", f"{L}.ln_2", src="X", dst="Xn8", extra=dict(out_scale=sc["ln_2"])))
+        self.steps.append(Step("f8", f"{L}.mlp.0", F8Linear(
+            f"{L}.mlp.0", p[f"{L}.mlp.0.weight"], p[f"{L}.mlp.0.bias"], sc["ln_2"], relu_out=3, device=dev),
+            "Xn8", "Hd8", extra=dict(out_scale=sc["gelu"])))
+        self.steps.append(Step("f8", f"{L}.mlp.3", F8Linear(
+            f"{L}.mlp.3", p[f"{L}.mlp.3.weight"], p[f"{L}.mlp.3.bias"], sc["gelu"], device=dev), "Hd8", "X",
+            res="X"))
+
     def _alloc(self) -> None:
         B, S, dev, D, T = self.max_batch, self.size, self.device, V.DIM, self.T
         self.inp = torch.zeros((B, S, S, 3), dtype=torch.uint8, device=dev)
@@ -95,12 +137,26 @@ class ViTEngine(EngineBase):
                      "QKV": z(B * T, 3 * D), "A": z(B * T, D), "Hd": z(B * T, V.MLP),
                      "CLS": z((B + 15) // 16 * 16, D)}
         self.ld = {"patches": D, "X": D, "Xn": D, "QKV": 3 * D, "A": D, "Hd": V.MLP, "CLS": D}
+        if self.fp8:
+            u8 = lambda *shape: torch.zeros(*shape, dtype=torch.uint8, device=dev)  # noqa: E731
+            self.bufs.update({"Xn8": u8(B * T, D), "A8": u8(B * T, D), "Hd8": u8(B * T, V.MLP)})
+            self.ld.update({"Xn8": D, "A8": D, "Hd8": V.MLP})
         self.logits = torch.zeros((B, self.classes), dtype=torch.float32, device=dev)
 
     def _ptr(self, name: str) -> int:
         return _lib.ptr(self.bufs[name])
 
     def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
+        if step.kind == "f8":
+            out_scale = step.extra.get("out_scale")
+            kw = dict(x8=self._ptr(step.src), M=b * self.T, res=self._ptr(step.res) if step.res else None,
+                      ldy=self.ld[step.dst])
+            if out_scale is not None:
+                kw.update(y8=self._ptr(step.dst), out_scale=out_scale)
+            else:
+                kw.update(y=self._ptr(step.dst))
+            step.layer.emit(prog, cfg=cfg, **kw)
+            return
         lay: ConvGemmLayer = step.layer
         if step.extra.get("kind") == "patch":
             g = Geometry(b, V.INPUT_SIZE // V.PATCH, V.INPUT_SIZE // V.PATCH,
@@ -125,7 +181,7 @@ class ViTEngine(EngineBase):
             prog.add_patchify(step.name, dict(x=self.input_ptr(), y=self._ptr("patches"), B=b, H=self.size,
                                               W=self.size, P=V.PATCH, ldy=D, scale0=sc[0], scale1=sc[1],
                                               scale2=sc[2], shift0=sh[0], shift1=sh[1], shift2=sh[2]))
-        elif step.kind == "conv":
+        elif step.kind in ("conv", "f8"):
             self._emit_conv(prog, step, b)
         elif step.kind == "embed":
             prog.add_embed(step.name, dict(x=self._ptr("X"), cls=_lib.ptr(self.cls), pos=_lib.ptr(self.pos),
@@ -137,12 +193,15 @@ class ViTEngine(EngineBase):
                                                    beta=_lib.ptr(bb), rows=b, D=D, ldx=self.T * D, ldy=D,
                                                    eps=V.LN_EPS))
             else:
-                prog.add_layernorm(step.name, dict(x=self._ptr(step.src), y=self._ptr(step.dst), gamma=_lib.ptr(g),
-                                                   beta=_lib.ptr(bb), rows=b * self.T, D=D, ldx=D, ldy=D,
-                                                   eps=V.LN_EPS))
+                osc = step.extra.get("out_scale")
+                out = dict(y8=self._ptr(step.dst), inv_scale=1.0 / osc) if osc else dict(y=self._ptr(step.dst))
+                prog.add_layernorm(step.name, dict(x=self._ptr(step.src), gamma=_lib.ptr(g), beta=_lib.ptr(bb),
+                                                   rows=b * self.T, D=D, ldx=D, ldy=D, eps=V.LN_EPS, **out))
         elif step.kind == "attn":
-            prog.add_attention(step.name, dict(qkv=self._ptr("QKV"), out=self._ptr("A"), B=b, T=self.T,
-                                               H=V.HEADS, dh=D // V.HEADS, scale=(D // V.HEADS) ** -0.5))
+            osc = step.extra.get("out_scale")
+            out = dict(out8=self._ptr(step.dst), inv_scale=1.0 / osc) if osc else dict(out=self._ptr(step.dst))
+            prog.add_attention(step.name, dict(qkv=self._ptr("QKV"), B=b, T=self.T, H=V.HEADS, dh=D // V.HEADS,
+                                               scale=(D // V.HEADS) ** -0.5, **out))
         elif step.kind == "fc":
             prog.add_fc_mfma(step.name, dict(xb=self._ptr("CLS"), wp=_lib.ptr(self.head_wp),
                                              bias=_lib.ptr(self.head_b), out=_lib.ptr(self.logits), B=b, F=D,

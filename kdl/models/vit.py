@@ -120,6 +120,29 @@ def vit_forward(p, x_u8_nhwc: torch.Tensor) -> torch.Tensor:
     return c @ p["heads.head.weight"].t() + p["heads.head.bias"]
 
 
+@torch.no_grad()
+def activation_amax(p, x_u8_nhwc: torch.Tensor) -> list[dict[str, float]]:
+    """Calibration for the fp8 engine: per encoder layer, the max |value| of the four
+    tensors that feed fp8 GEMMs (ln_1 out -> QKV, attention out -> out_proj,
+    ln_2 out -> mlp.0, GELU out -> mlp.3)."""
+    out = []
+    x = embed(p, preprocess(x_u8_nhwc))
+    for i in range(DEPTH):
+        L = _layer(i)
+        h1 = F.layer_norm(x, (DIM,), p[f"{L}.ln_1.weight"], p[f"{L}.ln_1.bias"], LN_EPS)
+        B, N, D = h1.shape
+        qkv = h1 @ p[f"{L}.self_attention.in_proj_weight"].t() + p[f"{L}.self_attention.in_proj_bias"]
+        q, k, v = qkv.view(B, N, 3, HEADS, D // HEADS).permute(2, 0, 3, 1, 4)
+        a = (torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(D // HEADS), dim=-1) @ v).transpose(1, 2).reshape(B, N, D)
+        x = x + a @ p[f"{L}.self_attention.out_proj.weight"].t() + p[f"{L}.self_attention.out_proj.bias"]
+        h2 = F.layer_norm(x, (DIM,), p[f"{L}.ln_2.weight"], p[f"{L}.ln_2.bias"], LN_EPS)
+        g = F.gelu(h2 @ p[f"{L}.mlp.0.weight"].t() + p[f"{L}.mlp.0.bias"])
+        x = x + g @ p[f"{L}.mlp.3.weight"].t() + p[f"{L}.mlp.3.bias"]
+        out.append({"ln_1": h1.abs().max().item(), "attn": a.abs().max().item(),
+                    "ln_2": h2.abs().max().item(), "gelu": g.abs().max().item()})
+    return out
+
+
 def macs_per_image() -> int:
     n = TOKENS
     per_layer = n * DIM * 3 * DIM + 2 * n * n * DIM + n * DIM * DIM + 2 * n * DIM * MLP
