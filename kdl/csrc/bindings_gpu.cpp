@@ -30,6 +30,7 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.wp = P<const uint16_t>(d, "wp");
   a.bias = P<const float>(d, "bias");
   a.dww = P<const float>(d, "dww");
+  a.dwk = P<const float>(d, "dwk");
   a.res = P<const uint16_t>(d, "res");
   a.y = P<uint16_t>(d, "y");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W");
@@ -190,6 +191,7 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(bm, bn, th);
   });
   m.def("conv_gemm_num_configs", &conv_gemm_num_configs);
+  m.def("sepconv_pipe_fits", &sepconv_pipe_fits);
   m.def("dw3x3", [](py::dict d, uintptr_t s) {
     const auto a = dw_args(d);
     py::gil_scoped_release nogil;

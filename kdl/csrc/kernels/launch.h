@@ -12,6 +12,7 @@ struct ConvGemmArgs {
   const uint16_t* wp;    // packed weights [NF][K/32][64][8] bf16 (BN scale folded)
   const float* bias;     // [NF*16] fp32 (BN shift)
   const float* dww;      // MODE_DW: depthwise weights [9][K] fp32
+  const float* dwk;      // MODE_DW, sepconv_pipe: the same weights packed [K/32][9][32]
   const uint16_t* res;   // optional residual [M][ldr] bf16
   uint16_t* y;           // output [M][ldy] bf16 (or a zero-bordered [B][OH+2][OW+2][ldy] if opad)
   int B, H, W;           // input spatial dims
@@ -37,6 +38,11 @@ constexpr int PIPE_CFG_BASE = 16;
 // cfg >= SEP_CFG_BASE: fused separable conv (MODE_DW only, sepconv_fused.hip).
 constexpr int SEP_CFG_BASE = 64;
 hipError_t sepconv_fused(int cfg, const ConvGemmArgs& a, hipStream_t s);
+// cfg >= SEPP_CFG_BASE: LDS-DMA pipelined fused separable conv (MODE_DW only, sepconv_pipe.hip).
+constexpr int SEPP_CFG_BASE = 96;
+hipError_t sepconv_pipe(int cfg, const ConvGemmArgs& a, hipStream_t s);
+int sepconv_pipe_config(int cfg, int* bm, int* bn, int* threads);
+int sepconv_pipe_fits(int cfg, int W);
 int sepconv_fused_config(int cfg, int* bm, int* bn, int* threads);
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);

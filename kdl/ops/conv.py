@@ -34,16 +34,25 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            # ids >= SEP_BASE: fused separable conv (sepconv_fused.hip): (FM, NFW, 1, NW)
            64: (4, 6, 1, 8), 65: (4, 1, 1, 8), 66: (4, 2, 1, 8), 67: (2, 6, 1, 8), 68: (4, 4, 1, 8),
            69: (4, 3, 1, 8), 70: (8, 1, 1, 8), 71: (8, 2, 1, 8), 72: (2, 3, 1, 8), 73: (4, 2, 1, 4),
-           74: (4, 1, 1, 4)}
+           74: (4, 1, 1, 4),
+           # ids >= SEPP_BASE: LDS-DMA pipelined fused separable conv (sepconv_pipe.hip)
+           96: (3, 6, 2, 4), 97: (3, 6, 2, 4), 98: (3, 3, 2, 4), 99: (2, 6, 2, 4), 100: (3, 3, 2, 4),
+           101: (2, 3, 2, 4), 102: (2, 6, 2, 4), 103: (3, 3, 2, 4), 104: (2, 3, 2, 4)}
 SEP_BASE = 64
+SEPP_BASE = 96
+# x-band KiB per stage of each KDL_SEPP_CONFIGS entry (mirror of sepconv_pipe_fits)
+SEPP_XB = {96: 11, 97: 11, 98: 11, 99: 9, 100: 11, 101: 9, 102: 17, 103: 19, 104: 17}
 # staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
 SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
 
 
 def config_applicable(cfg: int, W: int | None) -> bool:
-    """Mirror of the host-side launch checks in sepconv_fused.hip."""
+    """Mirror of the host-side launch checks in sepconv_fused.hip / sepconv_pipe.hip."""
     if cfg < SEP_BASE or W is None:
         return True
+    if cfg >= SEPP_BASE:
+        bm = cfg_tile(cfg)[0]
+        return ((bm + W - 2) // W + 3) * W * 4 <= SEPP_XB[cfg] * 64
     fm, nfw, _, nw = CONFIGS[cfg]
     bm, bn = 16 * fm, 16 * nfw * nw
     maxr = (bm - 1) // W + 4
@@ -118,9 +127,12 @@ class ConvGemmLayer:
         self.wp = pack_fragments(w_nk, self.nf_max, self.K // 32).to(device).contiguous()
         self.bias = pad_vec(bias, self.nf_max * 16).to(device)
         self.dww = None
+        self.dwk = None
         if mode == MODE_DW:
             assert dww is not None and dww.shape == (9, cin_pad)
             self.dww = dww.float().contiguous().to(device)
+            # [K/32][9][32]: one contiguous 1152-byte block per k-step (sepconv_pipe stages it by LDS-DMA)
+            self.dwk = dww.float().view(9, cin_pad // 32, 32).permute(1, 0, 2).contiguous().to(device)
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
         self.w_ref = w_nk.to(torch.bfloat16).float()
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
@@ -173,7 +185,7 @@ class ConvGemmLayer:
     def args(self, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
              ldr: int | None = None, cfg: int | None = None, opad: int = 0) -> dict:
         return dict(x=x, wp=_lib.ptr(self.wp), bias=_lib.ptr(self.bias),
-                    dww=_lib.ptr(self.dww), res=res, y=y,
+                    dww=_lib.ptr(self.dww), dwk=_lib.ptr(self.dwk), res=res, y=y,
                     B=g.B, H=g.H, W=g.W, OH=g.OH, OW=g.OW, M=g.M,
                     ldx=ldx if ldx is not None else self.cin_pad, ldy=self.ldy,
                     ldr=ldr if ldr is not None else self.ldy,

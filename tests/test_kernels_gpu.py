@@ -100,7 +100,10 @@ def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
         y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
         lay.launch(x, y, g, res=res, cfg=cfg, split=split)
         torch.cuda.synchronize()
-        _check(y, ref, n)
+        try:
+            _check(y, ref, n)
+        except AssertionError as e:
+            raise AssertionError(f"split={split} cfg={cfg}: {e}") from None
 
 
 def test_conv_gemm_repeat_race_screen():
