@@ -30,9 +30,10 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.wp = P<const uint16_t>(d, "wp");
   a.bias = P<const float>(d, "bias");
   a.dww = P<const float>(d, "dww");
-  a.dwk = P<const float>(d, "dwk");
+  a.dwk = P<const uint16_t>(d, "dwk");
   a.res = P<const uint16_t>(d, "res");
   a.y = P<uint16_t>(d, "y");
+  a.stamps = P<unsigned long long>(d, "stamps");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W");
   a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.M = I(d, "M");
   a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");

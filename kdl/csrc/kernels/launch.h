@@ -12,7 +12,8 @@ struct ConvGemmArgs {
   const uint16_t* wp;    // packed weights [NF][K/32][64][8] bf16 (BN scale folded)
   const float* bias;     // [NF*16] fp32 (BN shift)
   const float* dww;      // MODE_DW: depthwise weights [9][K] fp32
-  const float* dwk;      // MODE_DW, sepconv_pipe: the same weights packed [K/32][9][32]
+  const uint16_t* dwk;   // MODE_DW, sepconv_pipe: the same weights as bf16 entries [K/32][2][16][2][8]
+                         //   (k-step, channel group, channel, tap parity, taps parity+2j)
   const uint16_t* res;   // optional residual [M][ldr] bf16
   uint16_t* y;           // output [M][ldy] bf16 (or a zero-bordered [B][OH+2][OW+2][ldy] if opad)
   int B, H, W;           // input spatial dims
@@ -27,6 +28,7 @@ struct ConvGemmArgs {
   int relu_in;
   int relu_out;          // 0 none; 1 ReLU before the residual add (Xception); 2 after it (ResNet);
                          // 3 exact GELU before the residual add (ViT MLP); 4 SiLU before it (EfficientNet)
+  unsigned long long* stamps;  // diagnostics only (stamping kernel variants): per-wave s_memtime per k-step
   int opad;              // 1: write into the interior of a 1-pixel zero-bordered output buffer, so the
                          //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
                          // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
@@ -43,6 +45,9 @@ constexpr int SEPP_CFG_BASE = 96;
 hipError_t sepconv_pipe(int cfg, const ConvGemmArgs& a, hipStream_t s);
 int sepconv_pipe_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_pipe_fits(int cfg, int W);
+hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);     // ids SEPP_CFG_BASE + 24 ..
+int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
+int sepconv_ws_fits(int cfg, int W);
 int sepconv_fused_config(int cfg, int* bm, int* bn, int* threads);
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);

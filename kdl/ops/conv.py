@@ -36,12 +36,24 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            69: (4, 3, 1, 8), 70: (8, 1, 1, 8), 71: (8, 2, 1, 8), 72: (2, 3, 1, 8), 73: (4, 2, 1, 4),
            74: (4, 1, 1, 4),
            # ids >= SEPP_BASE: LDS-DMA pipelined fused separable conv (sepconv_pipe.hip)
-           96: (3, 6, 2, 4), 97: (3, 6, 2, 4), 98: (3, 3, 2, 4), 99: (2, 6, 2, 4), 100: (3, 3, 2, 4),
-           101: (2, 3, 2, 4), 102: (2, 6, 2, 4), 103: (3, 3, 2, 4), 104: (2, 3, 2, 4)}
+           96: (3, 6, 2, 4), 97: (3, 6, 2, 4), 98: (3, 3, 2, 4), 99: (2, 6, 2, 4), 100: (3, 6, 2, 4),
+           101: (3, 3, 2, 4), 102: (2, 6, 2, 4), 103: (2, 3, 2, 4), 104: (3, 3, 2, 4),
+           # timing ablations of 97 (tools/kbench.py --cfgs; never candidates)
+           112: (3, 6, 2, 4), 113: (3, 6, 2, 4), 114: (3, 6, 2, 4), 115: (3, 6, 2, 4), 116: (3, 6, 2, 4),
+           117: (3, 6, 2, 4),
+           # warp-specialized fused separable conv (sepconv_ws.hip): (FM, FN, 1, 4)
+           120: (6, 6, 1, 4), 121: (6, 6, 1, 4), 122: (6, 6, 1, 4), 123: (6, 6, 1, 4), 124: (6, 3, 1, 4),
+           125: (4, 6, 1, 4), 126: (6, 6, 1, 4), 127: (6, 6, 1, 4),
+           128: (6, 6, 1, 4), 129: (6, 6, 1, 4), 130: (6, 6, 1, 4),
+           131: (6, 6, 1, 4), 132: (6, 6, 1, 4), 133: (6, 6, 1, 4), 134: (6, 6, 1, 4)}
 SEP_BASE = 64
 SEPP_BASE = 96
+SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
 # x-band KiB per stage of each KDL_SEPP_CONFIGS entry (mirror of sepconv_pipe_fits)
-SEPP_XB = {96: 11, 97: 11, 98: 11, 99: 9, 100: 11, 101: 9, 102: 17, 103: 19, 104: 17}
+SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 104: 12,
+           **{i: 12 for i in range(112, 118)},
+           120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9, 128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 134: 9}
+ABLATION_IDS = frozenset(list(range(112, 118)) + list(range(127, 135)))   # 127+: s_memtime stamping
 # staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
 SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
 
@@ -50,9 +62,11 @@ def config_applicable(cfg: int, W: int | None) -> bool:
     """Mirror of the host-side launch checks in sepconv_fused.hip / sepconv_pipe.hip."""
     if cfg < SEP_BASE or W is None:
         return True
+    if cfg >= SEPW_BASE:
+        return cfg_tile(cfg)[0] + 2 * W + 3 <= SEPP_XB[cfg] * 16
     if cfg >= SEPP_BASE:
         bm = cfg_tile(cfg)[0]
-        return ((bm + W - 2) // W + 3) * W * 4 <= SEPP_XB[cfg] * 64
+        return ((bm + W - 2) // W + 3) * W + 1 <= SEPP_XB[cfg] * 16
     fm, nfw, _, nw = CONFIGS[cfg]
     bm, bn = 16 * fm, 16 * nfw * nw
     maxr = (bm - 1) // W + 4
@@ -69,7 +83,7 @@ def cfg_tile(cfg: int) -> tuple[int, int]:
 
 def candidate_configs(n: int, m: int | None = None) -> list[int]:
     """Configs whose N tile does not waste more than ~35% of the channels."""
-    ids = sorted(CONFIGS)
+    ids = sorted(c for c in CONFIGS if c not in ABLATION_IDS)
     out = [c for c in ids if round_up(n, cfg_tile(c)[1]) <= 1.35 * round_up(n, 16)]
     if not out:  # tiny N: smallest N tile only
         bn_min = min(cfg_tile(c)[1] for c in ids)
@@ -131,8 +145,7 @@ class ConvGemmLayer:
         if mode == MODE_DW:
             assert dww is not None and dww.shape == (9, cin_pad)
             self.dww = dww.float().contiguous().to(device)
-            # [K/32][9][32]: one contiguous 1152-byte block per k-step (sepconv_pipe stages it by LDS-DMA)
-            self.dwk = dww.float().view(9, cin_pad // 32, 32).permute(1, 0, 2).contiguous().to(device)
+            self.dwk = pack_dw_entries(dww).to(device)
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
         self.w_ref = w_nk.to(torch.bfloat16).float()
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
@@ -218,6 +231,18 @@ class ConvGemmLayer:
             assert g.OH == (g.H - 1) // self.stride + 1 and g.OW == (g.W - 1) // self.stride + 1
         if res is not None:
             assert res.dtype == torch.bfloat16 and res.numel() >= g.M * self.ldy
+
+
+def pack_dw_entries(dww: torch.Tensor) -> torch.Tensor:
+    """Depthwise weights [9][C] -> sepconv_pipe's per-k-step weight entries, bf16
+    [C/32][g 2][n 16][parity 2][8]: entry (g, n, p) holds w[p + 2j][32t + 16g + n] for
+    j = 0..4 (0 past tap 8), one 16-byte LDS read per lane (sepconv_pipe.hip)."""
+    C = dww.shape[1]
+    w = torch.cat([dww.float(), torch.zeros(1, C)], 0)          # taps 0..9
+    w = w.view(5, 2, C // 32, 2, 16)                           # [j][parity][t][g][n]
+    e = w.permute(2, 3, 4, 1, 0)                               # [t][g][n][parity][j]
+    e = torch.cat([e, torch.zeros(*e.shape[:-1], 3)], -1)      # j padded to 8
+    return e.to(torch.bfloat16).contiguous()
 
 
 def conv_weights_nk(kernel_hwio: torch.Tensor, cin_pad: int) -> torch.Tensor:

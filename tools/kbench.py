@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--top", type=int, default=6)
+    ap.add_argument("--cfgs", default=None, help="comma list of (fused) config ids to time instead of all variants; "
+                                                  "s<id> for the split lowering")
     a = ap.parse_args()
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
@@ -61,9 +63,12 @@ def main():
         y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device="cuda")
         macs = g.M * n * (9 * cin if mode == MODE_CONV else cin)
         tmp = torch.zeros(g.M * lay.cin_pad, dtype=torch.bfloat16, device="cuda")
-        times = {v: [] for v in lay.variants(H)}
+        variants = lay.variants(H)
+        if a.cfgs:
+            variants = [(c.startswith("s"), int(c.lstrip("s"))) for c in a.cfgs.split(",")]
+        times = {v: [] for v in variants}
         for _ in range(a.rounds):
-            for split, cfg in lay.variants(H):
+            for split, cfg in variants:
                 def run():
                     lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, tmp=_lib.ptr(tmp), split=split, cfg=cfg)
                 run()
