@@ -45,6 +45,7 @@ def main(argv=None) -> int:
     ap.add_argument("--ingress", choices=["scatter", "local"], default="scatter")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-tune", action="store_true")
+    ap.add_argument("--retune", action="store_true", help="autotune even if a tuning table exists")
     ap.add_argument("--profile-layers", action="store_true")
     ap.add_argument("--save-tuning", default=None, help="write the autotune result (rank 0) to this path")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # gloo: pipeline logic checks
@@ -74,7 +75,7 @@ def main(argv=None) -> int:
     params = info.init_params(0)
     eng = info.engine(params, B, dev)
     tp = tuning_path(a.model, B)
-    if tp.exists():
+    if tp.exists() and not a.retune:
         eng.load_tuning(tp)
     elif not a.no_tune:
         eng.autotune(B)
