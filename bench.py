@@ -44,6 +44,8 @@ def main(argv=None) -> int:
                     help="xception (headline) | resnet50 | vit_b16 | vit_b16_fp8 | efficientnet_b7")
     ap.add_argument("--ingress", choices=["scatter", "local"], default="scatter")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="ingress prefetch distance in batches (input slots = depth + 1)")
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--retune", action="store_true", help="autotune even if a tuning table exists")
     ap.add_argument("--profile-layers", action="store_true")
@@ -92,37 +94,38 @@ def main(argv=None) -> int:
     has_host = a.ingress == "local" or rank == 0
     host = (torch.randint(0, 256, (n_host, S, S, 3), generator=g, dtype=torch.uint8).pin_memory()
             if has_host else None)
-    # two engine input slots, each with its own captured graph: batch i+1 lands in one
-    # slot (H2D, or RCCL scatter) while batch i's graph reads the other
-    slots = eng.add_input_slots(2)
+    # NS engine slots (input + logits buffer, each with its own captured graph): batch
+    # i+depth lands in one slot (H2D, or RCCL scatter) and batch i-1's logits leave
+    # another while batch i's graph runs; no device-to-device copies anywhere.
+    NS = a.depth + 1
+    slots = eng.add_input_slots(NS)
     direct = world == 1 or a.ingress == "local"      # H2D straight into the slot
-    stage = ([torch.empty((n_host, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(2)]
-             if has_host and not direct else [None, None])
+    stage = ([torch.empty((n_host, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(NS)]
+             if has_host and not direct else [None] * NS)
     NC = info.classes
-    # per-slot device copy of the logits (the next graph overwrites eng.logits), the
-    # gathered logits and their pinned host copies; all double-buffered
-    lbuf = [torch.zeros((B, NC), dtype=torch.float32, device=dev) for _ in range(2)]
-    logits_all = [torch.zeros((n_global, NC), dtype=torch.float32, device=dev) for _ in range(2)]
-    out_host = [torch.zeros((n_global, NC), dtype=torch.float32).pin_memory() for _ in range(2)]
+    # gathered logits (rank 0, world > 1) and their pinned host copies, per slot
+    logits_all = [torch.zeros((n_global, NC), dtype=torch.float32, device=dev) for _ in range(NS)]
+    out_host = [torch.zeros((n_global, NC), dtype=torch.float32).pin_memory() for _ in range(NS)]
     s = eng.stream                          # compute: graph replays
     cs = torch.cuda.Stream(device=dev)      # ingress H2D
     ms = torch.cuda.Stream(device=dev)      # RCCL scatter / gather (overlaps the compute stream)
     ds = torch.cuda.Stream(device=dev)      # egress D2H
-    E = lambda: [torch.cuda.Event() for _ in range(2)]  # noqa: E731
-    ready, scattered, free, done, gathered, drained = E(), E(), E(), E(), E(), E()
-    for e in free + gathered + drained + scattered:
+    E = lambda: [torch.cuda.Event() for _ in range(NS)]  # noqa: E731
+    ready, scattered, free, done, drained = E(), E(), E(), E(), E()
+    for e in free + drained + scattered:
         e.record(s)
     total = a.warmup + a.steps
     t_in = [torch.cuda.Event(enable_timing=True) for _ in range(total + 1)]
     t_out = [torch.cuda.Event(enable_timing=True) for _ in range(total + 1)]
 
     # Software pipeline, one batch per step: while the graph of batch i runs on the
-    # compute stream, batch i+1 is H2D'd (copy stream) and RCCL-scattered (comm stream).
+    # compute stream, batch i+depth is H2D'd (copy stream) and RCCL-scattered (comm
+    # stream) and batch i-1's logits are gathered (comm) and copied out (egress).
     def ingress(i, timed=False):
-        j = i % 2
+        j = i % NS
         with torch.cuda.stream(cs):
-            cs.wait_event(free[j])          # slot j no longer read by the graph of batch i-2
-            cs.wait_event(scattered[j])     # stage j no longer read by the scatter of batch i-2
+            cs.wait_event(free[j])          # slot j no longer read by the graph of batch i-NS
+            cs.wait_event(scattered[j])     # stage j no longer read by the scatter of batch i-NS
             if timed:
                 t_in[i].record(cs)
             if has_host:
@@ -135,40 +138,38 @@ def main(argv=None) -> int:
                 scattered[j].record(ms)
 
     def compute(i):
-        j = i % 2
+        j = i % NS
         with torch.cuda.stream(s):
             s.wait_event(ready[j] if direct else scattered[j])
+            s.wait_event(drained[j])        # slot j's logits left (gather + D2H of batch i-NS)
             eng.launch(B, s, capture=use_graph, slot=j)
-            free[j].record(s)
-            s.wait_event(gathered[j])       # lbuf j no longer read by the gather of batch i-2
-            lbuf[j].copy_(eng.logits[:B])
-            done[j].record(s)
+            free[j].record(s)               # input and logits of slot j are final
 
     def collect(i, timed=False):
-        j = i % 2
-        with torch.cuda.stream(ms):
-            ms.wait_event(done[j])
-            ms.wait_event(drained[j])       # logits_all j no longer read by the D2H of batch i-2
-            if world > 1:
-                dist.gather(lbuf[j], list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
-            else:
-                logits_all[j].copy_(lbuf[j])
-            gathered[j].record(ms)
+        j = i % NS
+        out = eng.slot_logits(j)[:B]
+        src = out
+        if world > 1:
+            with torch.cuda.stream(ms):
+                ms.wait_event(free[j])
+                dist.gather(out, list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
+                done[j].record(ms)
+            src = logits_all[j]
         with torch.cuda.stream(ds):
-            ds.wait_event(gathered[j])
+            ds.wait_event(done[j] if world > 1 else free[j])
             if rank == 0:
-                out_host[j].copy_(logits_all[j], non_blocking=True)
+                out_host[j].copy_(src, non_blocking=True)
             drained[j].record(ds)
             if timed:
                 t_out[i].record(ds)
 
     def step(i):
-        ingress(i + 1)        # prefetch the next batch (K timed steps = K ingresses + K forwards)
+        ingress(i + a.depth)  # prefetch `depth` batches ahead (K timed steps = K ingresses + K forwards)
         compute(i)
         collect(i)
 
     # setup (not a warmup step): capture both slots' graphs and let the clocks ramp
-    for j in range(2):
+    for j in range(NS):
         eng.program(B, use_graph, j)
     t_settle = time.perf_counter() + a.settle
     while time.perf_counter() < t_settle:
@@ -177,7 +178,8 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    ingress(0)
+    for i in range(a.depth):
+        ingress(i)
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -188,6 +190,7 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     for i in range(a.warmup, total):
         step(i)
+    t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -243,6 +246,7 @@ def main(argv=None) -> int:
                        "ingress": a.ingress, "hipgraph": use_graph},
         }
         print(json.dumps(res), flush=True)
+        print(f"host issue time {t_issue * 1e3 / a.steps:.3f} ms/step", file=sys.stderr)
         if a.profile_layers:
             for name, t in eng.profile(B, 10):
                 print(f"{name:28s} {t * 1e3:9.1f} us", file=sys.stderr)

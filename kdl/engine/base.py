@@ -44,6 +44,7 @@ class EngineBase:
         self.programs: dict[tuple[int, bool, int], object] = {}
         self.stream = torch.cuda.Stream(device=self.device)
         self.inputs: list[torch.Tensor] = []   # input slots (self.inp is slot 0)
+        self.outputs: list[torch.Tensor] = []  # per-slot logits (self.logits is slot 0)
         self._slot = 0
 
     # ---------------------------------------------------------------- input slots
@@ -51,14 +52,24 @@ class EngineBase:
         """Device pointer of the input slot the program being built reads."""
         return _lib.ptr(self.inputs[self._slot] if self.inputs else self.inp)
 
+    def output_ptr(self) -> int:
+        """Device pointer of the logits buffer the program being built writes."""
+        return _lib.ptr(self.outputs[self._slot] if self.outputs else self.logits)
+
+    def slot_logits(self, slot: int) -> torch.Tensor:
+        return self.outputs[slot] if self.outputs else self.logits
+
     def add_input_slots(self, n: int) -> list[torch.Tensor]:
-        """Extra static input buffers, each with its own captured graphs, so a
-        pipelined caller can H2D batch i+1 into one slot while the graph of batch i
-        reads another (no device-to-device staging copy on the compute stream)."""
+        """Extra static input AND logits buffers, each slot with its own captured
+        graphs, so a pipelined caller can H2D batch i+1 into one slot while the graph
+        of batch i reads another, and D2H batch i's logits while batch i+1's graph
+        writes its own (no device-to-device copies on the compute stream)."""
         if not self.inputs:
             self.inputs = [self.inp]
+            self.outputs = [self.logits]
         while len(self.inputs) < n:
             self.inputs.append(torch.zeros_like(self.inp))
+            self.outputs.append(torch.zeros_like(self.logits))
         return self.inputs
 
     # ---------------------------------------------------------------- hooks

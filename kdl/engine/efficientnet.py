@@ -178,7 +178,7 @@ class EfficientNetEngine(EngineBase):
                                          ldx=E.HEAD, F=E.HEAD))
         elif step.kind == "fc":
             prog.add_fc_mfma(step.name, dict(xb=_lib.ptr(self.feat), wp=_lib.ptr(self.fc_wp),
-                                             bias=_lib.ptr(self.fc_b), out=_lib.ptr(self.logits), B=b, F=E.HEAD,
+                                             bias=_lib.ptr(self.fc_b), out=self.output_ptr(), B=b, F=E.HEAD,
                                              N=self.classes, NF=self.fc_nf, relu=0))
         else:  # pragma: no cover
             raise ValueError(step.kind)

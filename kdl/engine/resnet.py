@@ -127,7 +127,7 @@ class ResNetEngine(EngineBase):
         if name == "input":
             return self.input_ptr()
         if name == "logits":
-            return _lib.ptr(self.logits)
+            return self.output_ptr()
         if name == "feat":
             return _lib.ptr(self.feat)
         return _lib.ptr(self.bufs[name])

@@ -204,7 +204,7 @@ class ViTEngine(EngineBase):
                                                scale=(D // V.HEADS) ** -0.5, **out))
         elif step.kind == "fc":
             prog.add_fc_mfma(step.name, dict(xb=self._ptr("CLS"), wp=_lib.ptr(self.head_wp),
-                                             bias=_lib.ptr(self.head_b), out=_lib.ptr(self.logits), B=b, F=D,
+                                             bias=_lib.ptr(self.head_b), out=self.output_ptr(), B=b, F=D,
                                              N=self.classes, NF=self.head_nf, relu=0))
         else:  # pragma: no cover
             raise ValueError(step.kind)

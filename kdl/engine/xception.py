@@ -164,7 +164,7 @@ class XceptionEngine(EngineBase):
         if name == "input":
             return self.input_ptr()
         if name == "logits":
-            return _lib.ptr(self.logits)
+            return self.output_ptr()
         return _lib.ptr(self.bufs[name])
 
     def _emit(self, prog, step: Step, b: int) -> None:

@@ -29,6 +29,9 @@ SHAPES = {
     "mid_pw_k2": (MODE_PW, 1456, 728, 19, 1),
     "mid_pw_kh": (MODE_PW, 352, 728, 19, 1),
     "mid_pw_n2": (MODE_PW, 728, 1456, 19, 1),
+    # core-efficiency probes (large square GEMMs; M = batch*64*64)
+    "sq4k": (MODE_PW, 4096, 4096, 64, 1),
+    "sq2k": (MODE_PW, 2048, 2048, 64, 1),
 }
 
 
