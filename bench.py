@@ -25,6 +25,7 @@ import os
 import statistics
 import sys
 import time
+from pathlib import Path
 
 import torch
 import torch.distributed as dist
@@ -48,6 +49,7 @@ def main(argv=None) -> int:
                     help="ingress prefetch distance in batches (input slots = depth + 1)")
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--retune", action="store_true", help="autotune even if a tuning table exists")
+    ap.add_argument("--tuning", default=None, help="tuning table to load instead of kdl/tuning/<model>_b<batch>.json")
     ap.add_argument("--profile-layers", action="store_true")
     ap.add_argument("--save-tuning", default=None, help="write the autotune result (rank 0) to this path")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # gloo: pipeline logic checks
@@ -76,7 +78,7 @@ def main(argv=None) -> int:
     S = info.input_size
     params = info.init_params(0)
     eng = info.engine(params, B, dev)
-    tp = tuning_path(a.model, B)
+    tp = Path(a.tuning) if a.tuning else tuning_path(a.model, B)
     if tp.exists() and not a.retune:
         eng.load_tuning(tp)
     elif not a.no_tune:

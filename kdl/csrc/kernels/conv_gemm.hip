@@ -288,6 +288,7 @@ static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (a.K % 32 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (cfg >= S2D_CFG_BASE) return mode == MODE_DW ? sepconv_2d(cfg - S2D_CFG_BASE, a, s) : hipErrorInvalidValue;
   if (cfg >= SEPP_CFG_BASE) return mode == MODE_DW ? sepconv_pipe(cfg - SEPP_CFG_BASE, a, s) : hipErrorInvalidValue;
   if (cfg >= SEP_CFG_BASE) return mode == MODE_DW ? sepconv_fused(cfg - SEP_CFG_BASE, a, s) : hipErrorInvalidValue;
   if (cfg >= PIPE_CFG_BASE) return gemm_pipe(mode, cfg - PIPE_CFG_BASE, a, s);
@@ -300,6 +301,7 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
 }
 
 int conv_gemm_config(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg >= S2D_CFG_BASE) return sepconv_2d_config(cfg - S2D_CFG_BASE, bm, bn, threads);
   if (cfg >= SEPP_CFG_BASE) return sepconv_pipe_config(cfg - SEPP_CFG_BASE, bm, bn, threads);
   if (cfg >= SEP_CFG_BASE) return sepconv_fused_config(cfg - SEP_CFG_BASE, bm, bn, threads);
   if (cfg >= PIPE_CFG_BASE) return gemm_pipe_config(cfg - PIPE_CFG_BASE, bm, bn, threads);

@@ -49,6 +49,10 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);     // ids
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_ws_fits(int cfg, int W);
 int sepconv_fused_config(int cfg, int* bm, int* bn, int* threads);
+// cfg >= S2D_CFG_BASE: fused separable conv over 2-D spatial tiles (MODE_DW only, sepconv_2d.hip).
+constexpr int S2D_CFG_BASE = 160;
+hipError_t sepconv_2d(int cfg, const ConvGemmArgs& a, hipStream_t s);
+int sepconv_2d_config(int cfg, int* bm, int* bn, int* threads);
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads);

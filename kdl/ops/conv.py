@@ -45,10 +45,21 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            120: (6, 6, 1, 4), 121: (6, 6, 1, 4), 122: (6, 6, 1, 4), 123: (6, 6, 1, 4), 124: (6, 3, 1, 4),
            125: (4, 6, 1, 4), 126: (6, 6, 1, 4), 127: (6, 6, 1, 4),
            128: (6, 6, 1, 4), 129: (6, 6, 1, 4), 130: (6, 6, 1, 4),
-           131: (6, 6, 1, 4), 132: (6, 6, 1, 4), 133: (6, 6, 1, 4), 134: (6, 6, 1, 4)}
+           131: (6, 6, 1, 4), 132: (6, 6, 1, 4), 133: (6, 6, 1, 4), 134: (6, 6, 1, 4),
+           # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
+           160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
+           165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
+           170: (3, 2, 2, 4), 171: (2, 2, 2, 4), 172: (2, 2, 2, 4), 173: (3, 4, 2, 4),
+           # persistent 2-D tiled variant (sepconv_2dp_kernel, KDL_S2DP_CONFIGS): weights LDS-resident
+           184: (3, 2, 2, 4), 185: (2, 2, 2, 4), 186: (2, 4, 2, 4), 187: (4, 2, 2, 4), 188: (3, 2, 2, 4),
+           189: (2, 4, 2, 4)}
+# persistent 2-D variant: (STAGES, TH, TW) per id, mirror of KDL_S2DP_CONFIGS (LDS sizing)
+S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188: (6, 6, 16), 189: (4, 4, 16)}
 SEP_BASE = 64
 SEPP_BASE = 96
 SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
+S2D_BASE = 160    # 2-D spatial tiles (sepconv_2d.hip): the early flow's 147x147 / 74x74 maps
+S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 48, 19 -> 32)
 # x-band KiB per stage of each KDL_SEPP_CONFIGS entry (mirror of sepconv_pipe_fits)
 SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 104: 12,
            **{i: 12 for i in range(112, 118)},
@@ -58,10 +69,24 @@ ABLATION_IDS = frozenset(list(range(112, 118)) + list(range(127, 135)))   # 127+
 SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
 
 
-def config_applicable(cfg: int, W: int | None) -> bool:
-    """Mirror of the host-side launch checks in sepconv_fused.hip / sepconv_pipe.hip."""
+def s2dp_smem(cfg: int, K: int) -> int:
+    """LDS bytes of a persistent 2-D sepconv config (mirror of s2dp_smem in sepconv_2d.hip)."""
+    st, th, tw = S2DP[cfg]
+    bm, bn = cfg_tile(cfg)
+    ipp = ((th + 2) * (tw + 2) + 1 + 63) // 64
+    kt = K // 32
+    return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024 + bm * (bn * 2 + 16)
+
+
+def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | None = None) -> bool:
+    """Mirror of the host-side launch checks in sepconv_fused.hip / sepconv_pipe.hip / sepconv_2d.hip."""
     if cfg < SEP_BASE or W is None:
         return True
+    if cfg in S2DP:   # one N tile (all of N) with the whole K x N weight block resident in LDS
+        return (W >= S2D_MIN_W and (K is None or s2dp_smem(cfg, K) <= 160 * 1024)
+                and (n is None or round_up(n, cfg_tile(cfg)[1]) == cfg_tile(cfg)[1]))
+    if cfg >= S2D_BASE:
+        return W >= S2D_MIN_W
     if cfg >= SEPW_BASE:
         return cfg_tile(cfg)[0] + 2 * W + 3 <= SEPP_XB[cfg] * 16
     if cfg >= SEPP_BASE:
@@ -158,7 +183,7 @@ class ConvGemmLayer:
         if self.mode != MODE_DW:
             return [(False, c) for c in self.candidates if c < SEP_BASE]
         return ([(False, c) for c in self.candidates
-                 if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W)]
+                 if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W, self.K, self.n)]
                 + [(True, c) for c in self.candidates if c < SEP_BASE])
 
     def dw_args(self, x: int, tmp: int, g: Geometry, ldx: int | None = None) -> dict:

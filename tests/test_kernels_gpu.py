@@ -87,6 +87,10 @@ def test_conv_gemm_conv3x3():
     (64, 128, 29, False, True, False),
     (256, 728, 37, True, True, False),
     (1024, 1536, 10, False, True, False),
+    # 2-D spatial tiles (sepconv_2d.hip): partial tiles at both edges, with/without pre-ReLU
+    (64, 128, 74, False, True, False),
+    (128, 128, 67, True, False, True),
+    (256, 256, 70, True, True, False),
 ])
 def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
     gen = torch.Generator().manual_seed(3)
@@ -104,6 +108,25 @@ def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
             _check(y, ref, n)
         except AssertionError as e:
             raise AssertionError(f"split={split} cfg={cfg}: {e}") from None
+
+
+def test_sepconv_2d_repeat_race_screen():
+    """2-D tiled fused separable conv: run-to-run identical on an early-flow shape."""
+    gen = torch.Generator().manual_seed(5)
+    lay = _layer(MODE_DW, 128, 128, gen, relu_in=True, relu_out=False)
+    B, H = 4, 147
+    g = Geometry(B, H, H, H, H)
+    x = _rand_act((B, H, H), lay.cin_pad, 128, gen)
+    cfgs = [c for split, c in lay.variants(H) if not split and c >= 160]
+    assert cfgs, "no 2-D tiled variant offered at 147x147"
+    for cfg in cfgs:
+        y0 = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+        lay.launch(x, y0, g, cfg=cfg)
+        for _ in range(5):
+            y = torch.zeros_like(y0)
+            lay.launch(x, y, g, cfg=cfg)
+            torch.cuda.synchronize()
+            assert torch.equal(y, y0), f"cfg {cfg} nondeterministic"
 
 
 def test_conv_gemm_repeat_race_screen():

@@ -22,6 +22,8 @@ SHAPES = {
     "mid_pw": (MODE_PW, 728, 728, 19, 1),
     "b2_sep2": (MODE_DW, 128, 128, 147, 1),
     "b2_sep1": (MODE_DW, 64, 128, 147, 1),
+    "b3_sep1": (MODE_DW, 128, 256, 74, 1),
+    "b3_sep2": (MODE_DW, 256, 256, 74, 1),
     "b4_sep2": (MODE_DW, 728, 728, 37, 1),
     "b14_sep2": (MODE_DW, 1536, 2048, 10, 1),
     "stem2": (MODE_CONV, 32, 64, 149, 1),
