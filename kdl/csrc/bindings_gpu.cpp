@@ -153,6 +153,7 @@ HeadArgs head_args(const py::dict& d) {
   HeadArgs a{};
   a.x = P<const uint16_t>(d, "x"); a.w1 = P<const float>(d, "w1"); a.b1 = P<const float>(d, "b1");
   a.w2 = P<const float>(d, "w2"); a.b2 = P<const float>(d, "b2"); a.out = P<float>(d, "out");
+  a.feat = P<float>(d, "feat"); a.hid = P<float>(d, "hid");
   a.B = I(d, "B"); a.HW = I(d, "HW"); a.ldx = I(d, "ldx"); a.F = I(d, "F"); a.H1 = I(d, "H1");
   a.NC = I(d, "NC");
   return a;

@@ -228,11 +228,13 @@ hipError_t mfma_f8_probe(const void* a, const void* b, float* d, hipStream_t s);
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {
   const uint16_t* x;      // [B][HW][ldx] bf16
-  const float* w1;        // [F][H1] fp32 (Keras Dense kernel layout)
+  const float* w1;        // [H1][F] fp32 (the Keras [F][H1] Dense kernel, transposed at load)
   const float* b1;        // [H1]
   const float* w2;        // [H1][NC]
   const float* b2;        // [NC]
   float* out;             // [B][NC]
+  float* feat;            // scratch [B][F] fp32 (pooled features)
+  float* hid;             // scratch [F/64][B][H1] fp32 (dense1 K-split partials)
   int B, HW, ldx, F, H1, NC;
 };
 hipError_t head_dense(const HeadArgs& a, hipStream_t s);

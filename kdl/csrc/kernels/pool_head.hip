@@ -60,69 +60,154 @@ hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// One 1024-thread block per image (the head is latency-bound: parallelise every
-// reduction). GAP: 4 pixel groups x 256 channel-chunks, partial sums through LDS.
-// Dense1 (Keras [F][H1] layout, coalesced across outputs): 8 k-slices x 128
-// outputs, reduced through LDS. Dense2 is tiny.
-__global__ __launch_bounds__(1024) void head_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float hsm[];
-  float* part = hsm;                 // [4][F] GAP partials, later [8][128] dense partials
-  float* feat = hsm + 4 * a.F;       // [F]
-  float* hid = feat + a.F;           // [H1]
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const uint16_t* xb = a.x + (long)b * a.HW * a.ldx;
-  const int nchunk = a.F / 8;
-  for (int i = tid; i < 4 * nchunk; i += 1024) {
-    const int c8 = i % nchunk, pg = i / nchunk;
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 5
-    for (int p = pg; p < a.HW; p += 4) {
-      const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx + c8 * 8);
+// Classifier head as three small kernels. The head is bound by PER-CU bandwidth,
+// not by the chip: the previous one-block-per-image kernel put the whole 800 KB
+// Dense1 matrix through each of only 32 CUs (35-39 us at batch 32). Here
+//   gap_kernel    grid (B, F/256): 8 pixel groups x 32 channel chunks per block,
+//                 partial sums reduced through LDS -> feat [B][F] fp32;
+//   dense1_kernel grid F/64: K-split, w1 TRANSPOSED to [H1][F] at load time and read
+//                 once chip-wide -> partials [F/64][B][H1];
+//   dense2_kernel one block per image: partials (+b1, ReLU) and w2 in LDS, 16 lanes per logit.
+// Every sum is in a fixed order: deterministic logits.
+__global__ __launch_bounds__(256) void gap_kernel(HeadArgs a) {
+  __shared__ float part[8][256];
+  const int b = blockIdx.x, c0 = blockIdx.y * 256, tid = threadIdx.x;
+  const int c8 = tid & 31, pg = tid >> 5;       // 32 chunks of 8 channels x 8 pixel groups
+  const uint16_t* xb = a.x + (long)b * a.HW * a.ldx + c0 + c8 * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 + c8 * 8 < a.F) {
+#pragma unroll 16
+    for (int p = pg; p < a.HW; p += 8) {
+      const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         s[2 * d] += bf_lo(v[d]);
         s[2 * d + 1] += bf_hi(v[d]);
       }
     }
+  }
 #pragma unroll
-    for (int d = 0; d < 8; ++d) part[pg * a.F + c8 * 8 + d] = s[d];
+  for (int d = 0; d < 8; ++d) part[pg][c8 * 8 + d] = s[d];
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) t += part[g][tid];
+  if (c0 + tid < a.F) a.feat[(long)b * a.F + c0 + tid] = t * (1.0f / (float)a.HW);
+}
+
+// Dense1 split over K: block kb owns features [64kb, 64kb+64) for ALL images and ALL
+// hidden units, so w1 is read exactly once chip-wide and every block's operands sit in
+// LDS (w1 slice [H1][64], features [B][64]). Thread (o, image half) keeps 16 image
+// accumulators; the feature reads are wave-wide broadcasts, the w1 reads conflict-free
+// float4s. Partial sums go to part[kb][b][o]; dense2 reduces them in a fixed order.
+constexpr int D1_K = 64;
+__global__ __launch_bounds__(256) void dense1_kernel(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) float w1s[128][D1_K + 4];
+  __shared__ __attribute__((aligned(16))) float fs[64][D1_K];
+  const int kb = blockIdx.x, k0 = kb * D1_K, tid = threadIdx.x;
+  const int bb = blockIdx.y * 64;               // image block of this workgroup
+  const int bmax = min(a.B - bb, 64);
+  // staging: fixed trip counts, fully unrolled, so every load of a thread is in flight
+  // before its first LDS store (a strided loop paid one memory latency per iteration)
+  {
+    float4 wv[8], fv[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j, o = i / (D1_K / 4), c = i - o * (D1_K / 4);
+      wv[j] = o < a.H1 ? *(const float4*)(a.w1 + (long)o * a.F + k0 + c * 4) : (float4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + 256 * j, b = i / (D1_K / 4), c = i - b * (D1_K / 4);
+      fv[j] = b < bmax ? *(const float4*)(a.feat + (long)(bb + b) * a.F + k0 + c * 4) : (float4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j, o = i / (D1_K / 4), c = i - o * (D1_K / 4);
+      *(float4*)&w1s[o][c * 4] = wv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + 256 * j, b = i / (D1_K / 4), c = i - b * (D1_K / 4);
+      *(float4*)&fs[b][c * 4] = fv[j];
+    }
   }
   __syncthreads();
-  const float inv = 1.0f / (float)a.HW;
-  for (int k = tid; k < a.F; k += 1024)
-    feat[k] = (part[k] + part[a.F + k] + part[2 * a.F + k] + part[3 * a.F + k]) * inv;
-  __syncthreads();
+  // thread = 4 hidden units x 8 images: 12 LDS float4 reads feed 128 FMAs per k-quad
+  // (a thread per unit streaming every image was LDS-issue bound: 1 read per 4 FMAs)
+  const int ob = tid % 32, ib = tid / 32;       // 32 unit-quads x 8 image-octets
+  const int o0 = ob * 4, i0 = ib * 8;
+  if (o0 < a.H1 && i0 < bmax) {
+    float acc[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[r][i] = 0.f;
+#pragma unroll 2
+    for (int k = 0; k < D1_K; k += 4) {
+      float4 w[4], f[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = *(const float4*)&w1s[min(o0 + r, 127)][k];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = *(const float4*)&fs[min(i0 + i, 63)][k];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          acc[r][i] += w[r].x * f[i].x + w[r].y * f[i].y + w[r].z * f[i].z + w[r].w * f[i].w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (o0 + r < a.H1 && i0 + i < bmax) a.hid[((long)kb * a.B + bb + i0 + i) * a.H1 + o0 + r] = acc[r][i];
+  }
+}
+
+__global__ __launch_bounds__(256) void dense2_kernel(HeadArgs a) {
+  // one block per image: reduce dense1's K-split partials (+b1, ReLU) into LDS, then the
+  // logits with w2 staged in LDS, 16 lanes per logit
+  extern __shared__ __attribute__((aligned(16))) float d2s[];   // [H1] hid + [H1*NC] w2 + [2][128]
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nkb = a.F / D1_K;
+  float* hs = d2s;
+  float* w2s = d2s + a.H1;
+  // partials: 2 slices of the K-split per hidden unit per thread pair, all loads independent
+  float* red = w2s + a.H1 * a.NC;               // [2][128]
   {
-    const int o = tid & 127, sl = tid >> 7;   // 8 slices
-    const int klen = a.F / 8;
+    const int o = tid & 127, h = tid >> 7;
     float s = 0.f;
     if (o < a.H1) {
-      const float* w = a.w1 + (long)(sl * klen) * a.H1 + o;
-      const float* f = feat + sl * klen;
-#pragma unroll 8
-      for (int k = 0; k < klen; ++k) s += f[k] * w[(long)k * a.H1];
+#pragma unroll 16
+      for (int kb = h; kb < nkb; kb += 2) s += a.hid[((long)kb * a.B + b) * a.H1 + o];
     }
-    part[sl * 128 + o] = s;
+    red[h * 128 + o] = s;
   }
+#pragma unroll 4
+  for (int i = tid; i < a.H1 * a.NC; i += 256) w2s[i] = a.w2[i];
   __syncthreads();
-  if (tid < a.H1) {
-    float s = a.b1[tid];
-#pragma unroll
-    for (int sl = 0; sl < 8; ++sl) s += part[sl * 128 + tid];
-    hid[tid] = fmaxf(s, 0.f);
-  }
+  for (int o = tid; o < a.H1; o += 256) hs[o] = fmaxf(a.b1[o] + red[o] + red[128 + o], 0.f);
   __syncthreads();
-  if (tid < a.NC) {
-    float s = a.b2[tid];
-    for (int k = 0; k < a.H1; ++k) s += hid[k] * a.w2[(long)k * a.NC + tid];
-    a.out[(long)b * a.NC + tid] = s;
+  for (int o0 = 0; o0 < a.NC; o0 += 16) {
+    const int o = o0 + (tid >> 4), sl = tid & 15;
+    float s = 0.f;
+    if (o < a.NC)
+      for (int k = sl; k < a.H1; k += 16) s += hs[k] * w2s[k * a.NC + o];
+    s += __shfl_xor(s, 1, 16);
+    s += __shfl_xor(s, 2, 16);
+    s += __shfl_xor(s, 4, 16);
+    s += __shfl_xor(s, 8, 16);
+    if (o < a.NC && sl == 0) a.out[(long)b * a.NC + o] = s + a.b2[o];
   }
 }
 
 hipError_t head_dense(const HeadArgs& a, hipStream_t s) {
-  if (a.F % 64 != 0 || a.ldx % 8 != 0 || a.H1 > 128 || a.NC > 1024) return hipErrorInvalidValue;
-  const size_t smem = (size_t)(4 * a.F + a.F + a.H1) * sizeof(float);
-  hipLaunchKernelGGL(head_kernel, dim3(a.B), dim3(1024), smem, s, a);
+  if (a.F % D1_K != 0 || a.ldx % 8 != 0 || a.B <= 0 || a.H1 <= 0 || a.H1 > 128 || a.NC <= 0 ||
+      !a.feat || !a.hid)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gap_kernel, dim3(a.B, (a.F + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(dense1_kernel, dim3(a.F / D1_K, (a.B + 63) / 64), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(dense2_kernel, dim3(a.B), dim3(256), (size_t)(a.H1 + a.H1 * a.NC + 256) * sizeof(float), s, a);
   return hipGetLastError();
 }
 

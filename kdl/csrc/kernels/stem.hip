@@ -85,26 +85,35 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
       for (int j = 0; j < NF; ++j) acc[f][j] = mfma16(bw[j], af, acc[f][j]);
     }
   }
-  // lane holds Y[m_tile + (lane&15)][16j + 4*(lane>>4) + r]
+  // lane holds Y[m_tile + (lane&15)][16j + 4*(lane>>4) + r]. The block's 128 output
+  // pixels are consecutive rows of Y: stage the bf16 tile in LDS and write it back
+  // with coalesced 16-byte stores (8-byte per-lane stores scattered over 16 rows per
+  // instruction made this memory-bound kernel ~4x slower than its write volume).
+  __shared__ __attribute__((aligned(16))) uint16_t ys[128 * NF * 16];
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    const int mo = m_wave + f * 16 + (lane & 15);
-    if (mo < M) {
+    const int ml = wave * 32 + f * 16 + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < NF; ++j) {
-        const int n = 16 * j + 4 * (lane >> 4);
-        const float4 bv = *(const float4*)(a.bias + n);
-        float v0 = acc[f][j][0] + bv.x, v1 = acc[f][j][1] + bv.y;
-        float v2 = acc[f][j][2] + bv.z, v3 = acc[f][j][3] + bv.w;
-        if (a.relu == 1) {
-          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-        } else if (a.relu == 2) {
-          v0 = v0 / (1.f + __expf(-v0)); v1 = v1 / (1.f + __expf(-v1));
-          v2 = v2 / (1.f + __expf(-v2)); v3 = v3 / (1.f + __expf(-v3));
-        }
-        *(u32x2*)(a.y + (long)mo * a.ldy + n) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
+    for (int j = 0; j < NF; ++j) {
+      const int n = 16 * j + 4 * (lane >> 4);
+      const float4 bv = *(const float4*)(a.bias + n);
+      float v0 = acc[f][j][0] + bv.x, v1 = acc[f][j][1] + bv.y;
+      float v2 = acc[f][j][2] + bv.z, v3 = acc[f][j][3] + bv.w;
+      if (a.relu == 1) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      } else if (a.relu == 2) {
+        v0 = v0 / (1.f + __expf(-v0)); v1 = v1 / (1.f + __expf(-v1));
+        v2 = v2 / (1.f + __expf(-v2)); v3 = v3 / (1.f + __expf(-v3));
       }
+      *(u32x2*)(ys + ml * NF * 16 + n) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
     }
+  }
+  __syncthreads();
+  constexpr int CPR = NF * 2;                  // 16-byte chunks per output row
+  const int m0 = blockIdx.x * 128;
+  for (int c = threadIdx.x; c < 128 * CPR; c += 256) {
+    const int r = c / CPR, part = c - r * CPR;
+    if (m0 + r < M) *(u32x4*)(a.y + (long)(m0 + r) * a.ldy + part * 8) = *(const u32x4*)(ys + r * NF * 16 + part * 8);
   }
 }
 

@@ -115,12 +115,30 @@ class XceptionEngine(EngineBase):
                     cur = dst
         # --- head
         hd = self.head
-        self.w1 = p[f"{hd.hidden}/kernel"].float().contiguous().to(dev)   # Keras [F][H1]
+        self.w1 = p[f"{hd.hidden}/kernel"].float().t().contiguous().to(dev)   # Keras [F][H1] -> [H1][F]
         self.b1 = p[f"{hd.hidden}/bias"].float().to(dev)
         self.w2 = p[f"{hd.out}/kernel"].float().contiguous().to(dev)      # Keras [H1][NC]
         self.b2 = p[f"{hd.out}/bias"].float().to(dev)
         self.steps.append(Step("head", "head", src=cur, dst="logits", geom=(H, H, 1, 1)))
         self.feat_buf = cur
+        self._hoist_relus()
+
+    def _hoist_relus(self) -> None:
+        """Move each pre-activation ReLU of a separable conv into its producer's
+        epilogue when that producer's output feeds nothing else: relu(bf16(v)) ==
+        bf16(relu(v)), so results are bit-identical, and the ReLU runs once per output
+        element in the GEMM epilogue instead of once per depthwise tap read (9x, on the
+        VALU of the fused kernels and the dw3x3 staging). The block inputs of the
+        middle flow keep theirs: they are also the (pre-ReLU) residual."""
+        uses: dict[str, int] = {}
+        for st in self.steps:
+            for b in (st.src, st.res):
+                if b:
+                    uses[b] = uses.get(b, 0) + 1
+        for a, b in zip(self.steps, self.steps[1:]):
+            if (a.kind == "conv" and b.kind == "conv" and b.src == a.dst and uses.get(a.dst) == 1
+                    and a.res is None and a.layer.relu_out == 0 and b.layer.mode == MODE_DW and b.layer.relu_in):
+                a.layer.relu_out, b.layer.relu_in = 1, False
 
     @staticmethod
     def _pw(p, rc, dev) -> ConvGemmLayer:
@@ -151,6 +169,9 @@ class XceptionEngine(EngineBase):
         for name, (h, w, c) in self.shapes.items():
             self.bufs[name] = torch.zeros(B * h * w * c, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros((B, self.head.classes), dtype=torch.float32, device=dev)
+        self.head_feat = torch.zeros((B, self.head.features), dtype=torch.float32, device=dev)
+        self.head_hid = torch.zeros((self.head.features // 64, B, self.head.hidden_units), dtype=torch.float32,
+                                    device=dev)   # dense1 K-split partials
         # scratch for split separable convs (depthwise output), sized for the largest layer
         n = 1
         for st in self.conv_steps():
@@ -186,6 +207,7 @@ class XceptionEngine(EngineBase):
             prog.add_head(step.name, dict(x=self._ptr(step.src), w1=_lib.ptr(self.w1),
                                           b1=_lib.ptr(self.b1), w2=_lib.ptr(self.w2),
                                           b2=_lib.ptr(self.b2), out=self._ptr("logits"),
+                                          feat=_lib.ptr(self.head_feat), hid=_lib.ptr(self.head_hid),
                                           B=b, HW=H * W, ldx=self.shapes[step.src][2],
                                           F=hd.features, H1=hd.hidden_units, NC=hd.classes))
 

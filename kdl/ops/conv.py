@@ -106,18 +106,20 @@ def cfg_tile(cfg: int) -> tuple[int, int]:
     return 16 * fm * wgm, 16 * fn * wgn
 
 
-def candidate_configs(n: int, m: int | None = None) -> list[int]:
-    """Configs whose N tile does not waste more than ~35% of the channels."""
-    ids = sorted(c for c in CONFIGS if c not in ABLATION_IDS)
+def candidate_configs(n: int, m: int | None = None, mode: int | None = None) -> list[int]:
+    """Configs whose N tile does not waste more than ~35% of the channels (the fused
+    separable ids >= SEP_BASE only for MODE_DW layers)."""
+    ids = sorted(c for c in CONFIGS if c not in ABLATION_IDS and (mode is None or mode == MODE_DW or c < SEP_BASE))
     out = [c for c in ids if round_up(n, cfg_tile(c)[1]) <= 1.35 * round_up(n, 16)]
-    if not out:  # tiny N: smallest N tile only
-        bn_min = min(cfg_tile(c)[1] for c in ids)
-        out = [c for c in ids if cfg_tile(c)[1] == bn_min]
+    if not any(c < SEP_BASE for c in out):   # tiny N: always keep the plain GEMMs with the smallest N tile
+        plain = [c for c in ids if c < SEP_BASE]
+        bn_min = min(cfg_tile(c)[1] for c in plain)
+        out = sorted(out + [c for c in plain if cfg_tile(c)[1] == bn_min])
     return out
 
 
 def default_config(mode: int, n: int, m: int) -> int:
-    cands = candidate_configs(n, m)
+    cands = candidate_configs(n, m, mode)
     pref = [4, 6, 3, 2, 1, 0] if mode == MODE_DW else [16, 21, 18, 17, 19, 3, 6, 1, 2, 0]
     # (fused-separable ids are picked by the autotuner, which knows the image width)
     for c in pref:
@@ -158,7 +160,7 @@ class ConvGemmLayer:
         self.K = w_nk.shape[1]
         assert self.K % 32 == 0, (name, self.K)
         self.ldy = round_up(n, 32)
-        self.candidates = candidates if candidates is not None else candidate_configs(n)
+        self.candidates = candidates if candidates is not None else candidate_configs(n, mode=mode)
         self.nf_max = max(round_up(n, cfg_tile(c)[1]) // 16 for c in self.candidates)
         self.cfg = default_config(mode, n, 0) if candidates is None else self.candidates[0]
         if self.cfg not in self.candidates:

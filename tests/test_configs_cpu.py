@@ -1,0 +1,33 @@
+"""Tile-config tables (kdl.ops.conv): what each layer kind may be autotuned over."""
+import pytest
+
+from kdl.ops.conv import (CONFIGS, MODE_CONV, MODE_DW, MODE_PW, S2D_BASE, S2DP, SEP_BASE, candidate_configs,
+                          cfg_tile, config_applicable, s2dp_smem)
+
+
+@pytest.mark.parametrize("n", [8, 16, 32, 48, 64, 100, 128, 256, 728, 1024, 2048])
+@pytest.mark.parametrize("mode", [MODE_PW, MODE_CONV, MODE_DW])
+def test_candidates_valid_for_mode(n, mode):
+    c = candidate_configs(n, mode=mode)
+    assert c, "every layer needs at least one config"
+    assert any(x < SEP_BASE for x in c), "a plain GEMM / split path is always available"
+    if mode != MODE_DW:
+        assert all(x < SEP_BASE for x in c), "fused separable configs are MODE_DW only"
+
+
+def test_2d_configs_tile_shapes():
+    # sepconv_2d: M tile = TH x TW pixels with TW a multiple of 16
+    for cfg in range(S2D_BASE, S2D_BASE + 40):
+        if cfg in CONFIGS:
+            bm, bn = cfg_tile(cfg)
+            assert bm % 16 == 0 and bn % 16 == 0
+
+
+def test_persistent_lds_budget():
+    # the persistent 2-D variant keeps all K x N weights in LDS: K=128 fits, K=736 never does
+    for cfg in S2DP:
+        assert not config_applicable(cfg, 147, 736, cfg_tile(cfg)[1])
+    assert any(config_applicable(cfg, 147, 128, 128) for cfg in S2DP)
+    assert all(s2dp_smem(cfg, 64) < s2dp_smem(cfg, 128) for cfg in S2DP)
+    # too narrow a map for 16-pixel tile rows
+    assert not any(config_applicable(cfg, 37, 128, 128) for cfg in S2DP)

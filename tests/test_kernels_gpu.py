@@ -200,8 +200,11 @@ def test_head():
     w2 = (torch.randn(H1, NC, generator=gen) / 10).to(DEV)
     b2 = (torch.randn(NC, generator=gen) * 0.1).to(DEV)
     out = torch.zeros(B, NC, device=DEV)
-    _lib.lib().head_dense(dict(x=_lib.ptr(x), w1=_lib.ptr(w1), b1=_lib.ptr(b1), w2=_lib.ptr(w2),
-                               b2=_lib.ptr(b2), out=_lib.ptr(out), B=B, HW=HW, ldx=F_, F=F_, H1=H1, NC=NC),
+    w1t = w1.t().contiguous()
+    feat = torch.zeros(B, F_, device=DEV)
+    hid = torch.zeros(F_ // 64, B, H1, device=DEV)
+    _lib.lib().head_dense(dict(x=_lib.ptr(x), w1=_lib.ptr(w1t), b1=_lib.ptr(b1), w2=_lib.ptr(w2),
+                               b2=_lib.ptr(b2), out=_lib.ptr(out), feat=_lib.ptr(feat), hid=_lib.ptr(hid), B=B, HW=HW, ldx=F_, F=F_, H1=H1, NC=NC),
                           _lib.stream_ptr())
     torch.cuda.synchronize()
     ref = head_ref(x, B, HW, F_, F_, w1, b1, w2, b2)
