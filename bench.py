@@ -9,8 +9,12 @@ one dynamic batch of 32 images per GPU (weak scaling, global batch 32*N):
      on a copy stream;
   2. scatter: RCCL scatter of uint8 shards (4x fewer bytes than f32)
      on a comm stream, straight into one of every rank's two engine input slots;
-  3. forward: one hipGraph replay of the fused HIP-kernel model on the compute stream;
-  4. gather:  RCCL gather of the fp32 logits to rank 0 (comm stream), D2H (egress stream).
+  3. forward: hipGraph replays of the fused HIP-kernel model: for Xception the batch
+     runs as two concurrent 16-image lanes on two streams (``--lanes``,
+     kdl/engine/lanes.py), one lane's layer tails overlapping the other's body;
+  4. gather:  RCCL gather of the fp32 logits to rank 0 + D2H, both on the comm
+     stream (one GPU: D2H on an egress stream), so compute / lane / H2D / comm
+     streams each own one of the 4 hardware queues.
 Steps are software-pipelined: batch i+1's H2D + scatter overlap batch i's forward.
 
 ``--ingress local`` instead has every rank H2D its own shard (host-direct mode,
@@ -47,6 +51,9 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--depth", type=int, default=2,
                     help="ingress prefetch distance in batches (input slots = depth + 1)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="split each GPU's batch into this many concurrent hipGraph lanes "
+                         "(kdl/engine/lanes.py; default 2 for xception, 1 otherwise)")
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--retune", action="store_true", help="autotune even if a tuning table exists")
     ap.add_argument("--tuning", default=None, help="tuning table to load instead of kdl/tuning/<model>_b<batch>.json")
@@ -77,7 +84,13 @@ def main(argv=None) -> int:
     info = registry.get(a.model)
     S = info.input_size
     params = info.init_params(0)
-    eng = info.engine(params, B, dev)
+    if a.lanes is None:
+        a.lanes = 2 if a.model == "xception" and a.batch % 2 == 0 else 1
+    if a.lanes > 1:
+        from kdl.engine.lanes import LaneGroup
+        eng = LaneGroup(info, params, B, dev, a.lanes)
+    else:
+        eng = info.engine(params, B, dev)
     tp = Path(a.tuning) if a.tuning else tuning_path(a.model, B)
     if tp.exists() and not a.retune:
         eng.load_tuning(tp)
@@ -110,10 +123,10 @@ def main(argv=None) -> int:
     out_host = [torch.zeros((n_global, NC), dtype=torch.float32).pin_memory() for _ in range(NS)]
     s = eng.stream                          # compute: graph replays
     cs = torch.cuda.Stream(device=dev)      # ingress H2D
-    ms = torch.cuda.Stream(device=dev)      # RCCL scatter / gather (overlaps the compute stream)
-    ds = torch.cuda.Stream(device=dev)      # egress D2H
+    ms = torch.cuda.Stream(device=dev) if world > 1 else None   # RCCL scatter / gather + egress D2H
+    ds = torch.cuda.Stream(device=dev) if world == 1 else None  # egress D2H (one GPU)
     E = lambda: [torch.cuda.Event() for _ in range(NS)]  # noqa: E731
-    ready, scattered, free, done, drained = E(), E(), E(), E(), E()
+    ready, scattered, free, drained = E(), E(), E(), E()
     for e in free + drained + scattered:
         e.record(s)
     total = a.warmup + a.steps
@@ -150,17 +163,21 @@ def main(argv=None) -> int:
     def collect(i, timed=False):
         j = i % NS
         out = eng.slot_logits(j)[:B]
-        src = out
         if world > 1:
+            # gather + D2H on the comm stream: one fewer stream, so compute, lanes, H2D
+            # and comm each keep a hardware queue of their own (GPU_MAX_HW_QUEUES=4)
             with torch.cuda.stream(ms):
                 ms.wait_event(free[j])
                 dist.gather(out, list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
-                done[j].record(ms)
-            src = logits_all[j]
+                if rank == 0:
+                    out_host[j].copy_(logits_all[j], non_blocking=True)
+                drained[j].record(ms)
+                if timed:
+                    t_out[i].record(ms)
+            return
         with torch.cuda.stream(ds):
-            ds.wait_event(done[j] if world > 1 else free[j])
-            if rank == 0:
-                out_host[j].copy_(src, non_blocking=True)
+            ds.wait_event(free[j])
+            out_host[j].copy_(out, non_blocking=True)
             drained[j].record(ds)
             if timed:
                 t_out[i].record(ds)
@@ -245,7 +262,7 @@ def main(argv=None) -> int:
             "config": {"model": info.description,
                        "global_batch": n_global, "seq_len": None, "image_size": S,
                        "per_gpu_batch": B, "parallelism": f"dp{world}",
-                       "ingress": a.ingress, "hipgraph": use_graph},
+                       "ingress": a.ingress, "hipgraph": use_graph, "lanes": a.lanes},
         }
         print(json.dumps(res), flush=True)
         print(f"host issue time {t_issue * 1e3 / a.steps:.3f} ms/step", file=sys.stderr)

@@ -1,0 +1,119 @@
+"""Split-batch lanes: one logical batch-B engine made of L batch-B/L engines whose
+hipGraphs replay concurrently on L HIP streams.
+
+Why: the Xception forward is a chain of ~40 launches, and the small late-flow
+layers (19x19 maps, M = 32*361 rows) give each GEMM only ~250 workgroups, i.e.
+about one per CU on a 256-CU chip, so every layer ends in a tail where most CUs
+idle. Two or more independent half-batches on separate streams let one lane's
+tail overlap another lane's body (measured: `profiles/lanes_probe.txt`, +3-4 %
+on the graph alone). Each lane keeps the batch-B tile table (the tile choice is
+made for the combined occupancy, not for one lane alone).
+
+The group looks like an engine to `bench.py` and the serving executor: its
+input slots and per-slot logits are single contiguous [B, ...] tensors (one H2D
+or RCCL scatter per batch), and each lane's captured graph reads/writes its row
+range of them as views, so there are no device-to-device copies. ``launch``
+forks the caller's stream into the lanes with events and joins them back, so
+events recorded on the caller's stream afterwards cover every lane.
+
+The reference has no equivalent (TF-Serving runs one session per batch,
+`tf-serving.dockerfile:2-5`); this is MI355X occupancy engineering.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class LaneGroup:
+    def __init__(self, info, params: dict, max_batch: int, device, lanes: int):
+        assert lanes >= 1 and max_batch % lanes == 0, (max_batch, lanes)
+        self.device = torch.device(device)
+        self.max_batch = max_batch
+        self.lanes = lanes
+        self.b = max_batch // lanes
+        self.engines = [info.engine(params, self.b, self.device) for _ in range(lanes)]
+        e0 = self.engines[0]
+        self.stream = e0.stream
+        self.classes = e0.logits.shape[1]
+        self.inputs: list[torch.Tensor] = []
+        self.outputs: list[torch.Tensor] = []
+        self.add_input_slots(1)
+        self.inp, self.logits = self.inputs[0], self.outputs[0]
+        self._fork = [torch.cuda.Event() for _ in range(lanes)]
+        self._join = [torch.cuda.Event() for _ in range(lanes)]
+
+    # ---------------------------------------------------------------- tuning
+    def load_tuning(self, path) -> None:
+        for e in self.engines:
+            e.load_tuning(path)
+
+    def apply_tuning(self, d: dict) -> None:
+        for e in self.engines:
+            e.apply_tuning(d)
+
+    def tuning(self) -> dict:
+        return self.engines[0].tuning()
+
+    def save_tuning(self, path) -> None:
+        self.engines[0].save_tuning(path)
+
+    def autotune(self, b: int | None = None, **kw) -> dict:
+        t = self.engines[0].autotune(self.b, **kw)
+        for e in self.engines[1:]:
+            e.apply_tuning(t)
+        return t
+
+    # ---------------------------------------------------------------- slots
+    def add_input_slots(self, n: int) -> list[torch.Tensor]:
+        """Contiguous [B, ...] input / logits buffers per slot; lane k's graphs use
+        rows [k*b, (k+1)*b) of each (set before any program is built)."""
+        e0 = self.engines[0]
+        while len(self.inputs) < n:
+            self.inputs.append(torch.zeros((self.max_batch,) + tuple(e0.inp.shape[1:]),
+                                           dtype=e0.inp.dtype, device=self.device))
+            self.outputs.append(torch.zeros((self.max_batch, self.classes),
+                                            dtype=torch.float32, device=self.device))
+        for k, e in enumerate(self.engines):
+            r = slice(k * self.b, (k + 1) * self.b)
+            e.inputs = [x[r] for x in self.inputs]
+            e.outputs = [y[r] for y in self.outputs]
+            e.invalidate()
+        return self.inputs
+
+    def slot_logits(self, slot: int) -> torch.Tensor:
+        return self.outputs[slot]
+
+    # ---------------------------------------------------------------- execution
+    def program(self, b: int, capture: bool = True, slot: int = 0):
+        assert b == self.max_batch, "lanes run full batches only"
+        return [e.program(self.b, capture, slot) for e in self.engines]
+
+    def launch(self, b: int, stream: torch.cuda.Stream | None = None, capture: bool = True,
+               slot: int = 0) -> None:
+        """Lane 0 replays on ``stream``; lanes 1.. fork from it and join back into it."""
+        assert b == self.max_batch, "lanes run full batches only"
+        s = stream or self.stream
+        for k, e in enumerate(self.engines[1:], 1):
+            self._fork[k].record(s)
+            e.stream.wait_event(self._fork[k])
+            e.launch(self.b, e.stream, capture, slot)
+            self._join[k].record(e.stream)
+        self.engines[0].launch(self.b, s, capture, slot)
+        for k in range(1, self.lanes):
+            s.wait_event(self._join[k])
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, capture: bool = True) -> torch.Tensor:
+        n = x.shape[0]
+        assert n == self.max_batch, (n, self.max_batch)
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.inp.copy_(x, non_blocking=True)
+            self.launch(n, self.stream, capture)
+            out = self.logits.clone()
+        cur.wait_stream(self.stream)
+        return out
+
+    def profile(self, b: int, iters: int = 20):
+        return self.engines[0].profile(self.b, iters)

@@ -57,3 +57,26 @@ def test_bucket_padding_rows_do_not_leak(engine):
     b = engine.forward(img[:3])
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+def test_lane_group_matches_single_engine(xparams):
+    """Split-batch lanes (kdl/engine/lanes.py): two batch-2 graphs on two streams over
+    row views of one batch-4 slot give the single batch-4 engine's logits."""
+    from kdl.engine import registry
+    from kdl.engine.lanes import LaneGroup
+    from kdl.engine.xception import XceptionEngine
+    dev = torch.device("cuda", 0)
+    single = XceptionEngine(xparams, max_batch=4)
+    lanes = LaneGroup(registry.get("xception"), xparams, 4, dev, 2)
+    lanes.apply_tuning(single.tuning())
+    slots = lanes.add_input_slots(2)
+    gen = torch.Generator().manual_seed(13)
+    img = torch.randint(0, 256, (4, 299, 299, 3), generator=gen, dtype=torch.uint8)
+    ref = single.forward(img.cuda()).cpu()
+    slots[1].copy_(img.cuda())
+    torch.cuda.synchronize()
+    lanes.launch(4, lanes.stream, slot=1)
+    lanes.stream.synchronize()
+    out = lanes.slot_logits(1).cpu()
+    assert torch.allclose(out, ref, rtol=1e-3, atol=1e-3), (out, ref)
+    assert lanes.slot_logits(0).abs().sum().item() == 0.0   # slot 0 untouched
