@@ -9,8 +9,8 @@ one dynamic batch of 32 images per GPU (weak scaling, global batch 32*N):
      on a copy stream;
   2. scatter: RCCL scatter of uint8 shards (4x fewer bytes than f32)
      on a comm stream, straight into one of every rank's two engine input slots;
-  3. forward: hipGraph replays of the fused HIP-kernel model: for Xception the batch
-     runs as two concurrent 16-image lanes on two streams (``--lanes``,
+  3. forward: hipGraph replays of the fused HIP-kernel model: the batch runs as
+     two concurrent 16-image lanes on two streams (``--lanes``,
      kdl/engine/lanes.py), one lane's layer tails overlapping the other's body;
   4. gather:  RCCL gather of the fp32 logits to rank 0 + D2H, both on the comm
      stream (one GPU: D2H on an egress stream), so compute / lane / H2D / comm
@@ -53,7 +53,7 @@ def main(argv=None) -> int:
                     help="ingress prefetch distance in batches (input slots = depth + 1)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="split each GPU's batch into this many concurrent hipGraph lanes "
-                         "(kdl/engine/lanes.py; default 2 for xception, 1 otherwise)")
+                         "(kdl/engine/lanes.py; default 2 when the batch is even)")
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--retune", action="store_true", help="autotune even if a tuning table exists")
     ap.add_argument("--tuning", default=None, help="tuning table to load instead of kdl/tuning/<model>_b<batch>.json")
@@ -85,7 +85,7 @@ def main(argv=None) -> int:
     S = info.input_size
     params = info.init_params(0)
     if a.lanes is None:
-        a.lanes = 2 if a.model == "xception" and a.batch % 2 == 0 else 1
+        a.lanes = 2 if a.batch % 2 == 0 else 1
     if a.lanes > 1:
         from kdl.engine.lanes import LaneGroup
         eng = LaneGroup(info, params, B, dev, a.lanes)
