@@ -91,7 +91,9 @@ def main(argv=None) -> int:
         eng = LaneGroup(info, params, B, dev, a.lanes)
     else:
         eng = info.engine(params, B, dev)
-    tp = Path(a.tuning) if a.tuning else tuning_path(a.model, B)
+    tp = Path(a.tuning) if a.tuning else tuning_path(a.model, B, a.lanes)
+    if not a.tuning and not tp.exists():
+        tp = tuning_path(a.model, B)        # no lanes-tuned table: the single-lane one
     if tp.exists() and not a.retune:
         eng.load_tuning(tp)
     elif not a.no_tune:

@@ -57,11 +57,52 @@ class LaneGroup:
     def save_tuning(self, path) -> None:
         self.engines[0].save_tuning(path)
 
-    def autotune(self, b: int | None = None, **kw) -> dict:
-        t = self.engines[0].autotune(self.b, **kw)
-        for e in self.engines[1:]:
-            e.apply_tuning(t)
-        return t
+    def autotune(self, b: int | None = None, iters: int = 10, verbose: bool = False,
+                 concurrent: bool = False) -> dict:
+        """Per-layer tile choice. ``concurrent``: time each (split, cfg) variant with
+        every lane running the layer at once on its own stream (the lanes start
+        together and do identical work, so they stay roughly layer-aligned); the
+        winner is the variant that fills the chip best next to its twin, not the
+        fastest one alone. Off by default: on Xception b32 the concurrently tuned
+        table measured 17.2k img/s against 17.9k for the single-lane b32 table
+        (profiles/lanes_tuning_ab.txt) -- in the real graph the lanes drift out of
+        layer alignment, so the solo-fastest tile is the better proxy."""
+        if not concurrent or self.lanes == 1:
+            t = self.engines[0].autotune(self.b, iters=iters, verbose=verbose)
+            for e in self.engines[1:]:
+                e.apply_tuning(t)
+            return t
+        s0 = self.engines[0].stream
+        per_lane = [e.conv_steps() for e in self.engines]
+        chosen = {}
+        for idx, step in enumerate(per_lane[0]):
+            best = None
+            for split, cfg in self.engines[0]._variants(step):
+                def run():
+                    for e, steps in zip(self.engines, per_lane):
+                        with torch.cuda.stream(e.stream):
+                            e._emit_conv(None, steps[idx], self.b, split=split, cfg=cfg)
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                for rep in range(2):                  # rep 0 warms up
+                    t0.record(s0)
+                    for k, e in enumerate(self.engines[1:], 1):
+                        e.stream.wait_event(t0)
+                    for _ in range(2 if rep == 0 else iters):
+                        run()
+                    for k, e in enumerate(self.engines[1:], 1):
+                        self._join[k].record(e.stream)
+                        s0.wait_event(self._join[k])
+                    t1.record(s0)
+                    t1.synchronize()
+                t = t0.elapsed_time(t1) / iters
+                if best is None or t < best[0]:
+                    best = (t, split, cfg)
+                if verbose:
+                    print(f"  {step.name:24s} split={int(split)} cfg {cfg}: {t * 1e3:8.1f} us "
+                          f"({self.lanes} lanes)", flush=True)
+            chosen[step.name] = [int(best[1]), best[2]]
+        self.apply_tuning(chosen)
+        return chosen
 
     # ---------------------------------------------------------------- slots
     def add_input_slots(self, n: int) -> list[torch.Tensor]:
