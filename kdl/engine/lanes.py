@@ -25,13 +25,16 @@ import torch
 
 
 class LaneGroup:
-    def __init__(self, info, params: dict, max_batch: int, device, lanes: int):
+    def __init__(self, info, params: dict, max_batch: int, device, lanes: int, make=None):
+        """``make(b)``: optional engine factory (e.g. the serving executor's
+        Xception with a custom head / f32 input); default ``info.engine``."""
         assert lanes >= 1 and max_batch % lanes == 0, (max_batch, lanes)
         self.device = torch.device(device)
         self.max_batch = max_batch
         self.lanes = lanes
         self.b = max_batch // lanes
-        self.engines = [info.engine(params, self.b, self.device) for _ in range(lanes)]
+        make = make or (lambda b: info.engine(params, b, self.device))
+        self.engines = [make(self.b) for _ in range(lanes)]
         e0 = self.engines[0]
         self.stream = e0.stream
         self.classes = e0.logits.shape[1]

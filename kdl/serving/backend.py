@@ -244,15 +244,30 @@ class GPUExecutor(_Executor):
         bs = r.buckets
         in_kind = "u8" if r.sig.input_dtype == P.DT_UINT8 else "f32"
         dev = f"cuda:{self.device}"
-        if src.family == "xception":
-            from ..engine.xception import XceptionEngine
-            self.engine = XceptionEngine(src.params, max_batch=bs[-1], device=dev, in_kind=in_kind,
-                                         head=src.head, buckets=bs)
-        else:
-            self.engine = registry.get(src.family).engine(src.params, bs[-1], dev, buckets=bs)
+        def make(b, buckets=None):
+            if src.family == "xception":
+                from ..engine.xception import XceptionEngine
+                return XceptionEngine(src.params, max_batch=b, device=dev, in_kind=in_kind,
+                                      head=src.head, buckets=buckets)
+            return registry.get(src.family).engine(src.params, b, dev, buckets=buckets)
+        self.engine = make(bs[-1], bs)
         tp = tuning_path(src.family, bs[-1])
         if tp.exists():
             self.engine.load_tuning(tp)
+        # KDL_LANES=2: full batches of the top bucket run as concurrent split-batch
+        # lanes (kdl/engine/lanes.py, same tile table); smaller buckets use the engine.
+        # Off by default here: the closed-loop server is host-bound (one synchronous
+        # batch per executor) and the extra graph launch + fork/join cost 4 % at
+        # 16 clients x 8 images (profiles/serve_lanes_ab.txt), unlike bench.py.
+        self.lanes = None
+        nl = int(self.engine_kwargs.get("lanes", os.environ.get("KDL_LANES", "1")))
+        if nl > 1 and bs[-1] % nl == 0 and bs[-1] // nl >= 4:
+            from ..engine.lanes import LaneGroup
+            self.lanes = LaneGroup(None, None, bs[-1], dev, nl, make=make)
+            if tp.exists():
+                self.lanes.load_tuning(tp)
+            self.lanes.program(bs[-1], capture=True)
+            self.lanes.launch(bs[-1])
         dt = torch.uint8 if in_kind == "u8" else torch.float32
         S = src.input_size
         self.staging = torch.zeros((bs[-1], S, S, 3), dtype=dt).pin_memory()
@@ -266,7 +281,7 @@ class GPUExecutor(_Executor):
         return self.staging.data_ptr()
 
     def execute(self, bucket: int, n_real: int) -> int:
-        e = self.engine
+        e = self.lanes if self.lanes is not None and bucket == self.lanes.max_batch else self.engine
         with torch.cuda.stream(e.stream):
             e.inp[:bucket].copy_(self.staging[:bucket], non_blocking=True)
             e.launch(bucket, e.stream)

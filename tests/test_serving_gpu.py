@@ -90,3 +90,29 @@ def test_gpu_serving_other_families(tmp_path, family):
         assert torch.nn.functional.cosine_similarity(got, ref, dim=1).min() > 0.98
     finally:
         srv.stop(0)
+
+
+
+def test_gpu_server_lanes_path_matches_oracle(tmp_path, monkeypatch):
+    """KDL_LANES=2: a full top-bucket batch (16) runs on the executor's LaneGroup
+    (two 8-image hipGraph lanes, kdl/engine/lanes.py) and still matches the oracle."""
+    monkeypatch.setenv("KDL_LANES", "2")
+    base = tmp_path / "clothing-model"
+    (base / "1").mkdir(parents=True)
+    (base / "1" / "synthetic.json").write_text('{"seed": 0}')
+    cfg = ServerConfig(port=0, rest_api_port=0, model_base_path=str(base), device="gpu", gpus=1,
+                       host="127.0.0.1", file_system_poll_wait_seconds=0,
+                       batching=BatchingParams(max_batch_size=16, batch_timeout_micros=1000,
+                                               allowed_batch_sizes=[4, 16]))
+    srv = ModelServer(cfg).start(block_until_loaded=True)
+    try:
+        rng = np.random.default_rng(3)
+        u8 = rng.integers(0, 256, (16, 299, 299, 3), dtype=np.uint8)
+        stub = PredictionStub(grpc.insecure_channel(f"127.0.0.1:{srv.grpc_port}"))
+        r = stub.Predict(make_request(u8, signature="serving_uint8", input_key="images"), timeout=60)
+        got = np.asarray(r.outputs["dense_7"].float_val, np.float32).reshape(16, 10)
+    finally:
+        srv.stop(0)
+    x = torch.from_numpy(u8.astype(np.float32) / 127.5 - 1.0)
+    ref = X.xception_forward(X.init_params(seed=0), x).numpy()
+    assert np.abs(got - ref).max() < 0.05 * np.abs(ref).max()
