@@ -21,7 +21,18 @@ The reference has no equivalent (TF-Serving runs one session per batch,
 """
 from __future__ import annotations
 
+import os
+import warnings
+
 import torch
+
+
+def hw_queues() -> int:
+    """Hardware queues HIP gives this process (``GPU_MAX_HW_QUEUES``, HIP default 4)."""
+    try:
+        return max(1, int(os.environ.get("GPU_MAX_HW_QUEUES", "4")))
+    except ValueError:
+        return 4
 
 
 class LaneGroup:
@@ -29,6 +40,13 @@ class LaneGroup:
         """``make(b)``: optional engine factory (e.g. the serving executor's
         Xception with a custom head / f32 input); default ``info.engine``."""
         assert lanes >= 1 and max_batch % lanes == 0, (max_batch, lanes)
+        hwq = hw_queues()
+        if lanes + 1 > hwq:
+            # lanes + the ingress/egress stream must each keep a hardware queue: with
+            # GPU_MAX_HW_QUEUES=4, 4 lanes run at 12.0k vs 2 lanes 17.9k img/s
+            # (profiles/lanes4_vs2.txt) because streams start sharing queues.
+            warnings.warn(f"{lanes} lanes + 1 copy stream > GPU_MAX_HW_QUEUES={hwq}: "
+                          "streams will share hardware queues and serialise", stacklevel=2)
         self.device = torch.device(device)
         self.max_batch = max_batch
         self.lanes = lanes

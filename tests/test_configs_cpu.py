@@ -31,3 +31,17 @@ def test_persistent_lds_budget():
     assert all(s2dp_smem(cfg, 64) < s2dp_smem(cfg, 128) for cfg in S2DP)
     # too narrow a map for 16-pixel tile rows
     assert not any(config_applicable(cfg, 37, 128, 128) for cfg in S2DP)
+
+
+def test_lanes_hw_queue_budget(monkeypatch):
+    """Lanes + the copy stream must fit GPU_MAX_HW_QUEUES (profiles/lanes4_vs2.txt)."""
+    from kdl.engine.lanes import hw_queues
+
+    monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
+    assert hw_queues() == 4
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    assert hw_queues() == 8
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "junk")
+    assert hw_queues() == 4
+    # the default bench config (2 lanes + 1 copy stream) fits the default budget
+    assert 2 + 1 <= 4
