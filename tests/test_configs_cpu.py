@@ -34,7 +34,7 @@ def test_persistent_lds_budget():
 
 
 def test_lanes_hw_queue_budget(monkeypatch):
-    """Lanes + the copy stream must fit GPU_MAX_HW_QUEUES (profiles/lanes4_vs2.txt)."""
+    """GPU_MAX_HW_QUEUES parsing used by the lanes diagnostics (profiles/lanes4_vs2.txt)."""
     from kdl.engine.lanes import hw_queues
 
     monkeypatch.delenv("GPU_MAX_HW_QUEUES", raising=False)
@@ -43,5 +43,3 @@ def test_lanes_hw_queue_budget(monkeypatch):
     assert hw_queues() == 8
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "junk")
     assert hw_queues() == 4
-    # the default bench config (2 lanes + 1 copy stream) fits the default budget
-    assert 2 + 1 <= 4
