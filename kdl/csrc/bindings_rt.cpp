@@ -141,10 +141,13 @@ PYBIND11_MODULE(_rt, m) {
         if (size_t(info.size) * size_t(info.itemsize) < need) throw std::invalid_argument("payload smaller than n_items*item_bytes");
         return b.submit(reinterpret_cast<const uint8_t*>(info.ptr), n_items, deadline_us);
       })
+      // `out` may be larger than the ticket's n_items*out_cols floats, never smaller: a short
+      // buffer gets ST_ERROR and is left untouched (the C++ side checks the size it is given)
       .def("wait", [](DynamicBatcher& b, int64_t ticket, py::array_t<float, py::array::c_style> out) {
         float* p = out.mutable_data();
+        const size_t cap = size_t(out.size());
         py::gil_scoped_release nogil;
-        return b.wait(ticket, p);
+        return b.wait(ticket, p, cap);
       })
       .def("next_batch", [](DynamicBatcher& b, uintptr_t staging, int64_t poll_us) -> py::object {
         Batch batch;

@@ -46,7 +46,7 @@ int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadlin
   return r->ticket;
 }
 
-int DynamicBatcher::wait(int64_t ticket, float* out) {
+int DynamicBatcher::wait(int64_t ticket, float* out, size_t out_floats) {
   std::unique_lock<std::mutex> lk(mu_);
   auto it = live_.find(ticket);
   if (it == live_.end()) return ST_ERROR;
@@ -80,8 +80,11 @@ int DynamicBatcher::wait(int64_t ticket, float* out) {
     else
       cv_producer_.wait(lk);
   }
-  const int status = r->status;
-  if (status == ST_OK && out) std::memcpy(out, r->result.data(), r->result.size() * sizeof(float));
+  int status = r->status;
+  if (status == ST_OK && out) {
+    if (r->result.size() > out_floats) status = ST_ERROR;   // caller's buffer too small: never overrun it
+    else std::memcpy(out, r->result.data(), r->result.size() * sizeof(float));
+  }
   live_.erase(ticket);
   return status;
 }

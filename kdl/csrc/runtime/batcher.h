@@ -62,8 +62,9 @@ class DynamicBatcher {
   // `data` must stay valid until wait() returns for this ticket.
   int64_t submit(const uint8_t* data, int n_items, int64_t deadline_us);
   // Blocks until the request completes or its deadline passes; copies
-  // n_items*out_cols floats into `out`. Returns a BatchStatus.
-  int wait(int64_t ticket, float* out);
+  // n_items*out_cols floats into `out`, which holds `out_floats` floats (a smaller
+  // buffer is not written and the call returns ST_ERROR). Returns a BatchStatus.
+  int wait(int64_t ticket, float* out, size_t out_floats);
 
   // Consumer: waits up to poll_us for a batch; false on timeout/shutdown.
   bool next_batch(uint8_t* staging, int64_t poll_us, Batch* b);

@@ -45,7 +45,10 @@ Handle get_handle(const uint8_t*& p, const uint8_t* end) {
 
 // Block contents (decompressed) for a handle, checking the 5-byte trailer.
 std::string read_block(const std::string& file, Handle h, bool verify) {
-  if (h.offset + h.size + 5 > file.size()) throw std::runtime_error("sstable: block out of range");
+  // overflow-safe form of offset + size + 5 <= file.size() (the handle is untrusted)
+  const uint64_t fs = file.size();
+  if (h.size > fs || h.offset > fs - h.size || fs - h.offset - h.size < 5)
+    throw std::runtime_error("sstable: block out of range");
   const uint8_t* b = reinterpret_cast<const uint8_t*>(file.data()) + h.offset;
   const uint8_t type = b[h.size];
   if (verify) {
@@ -71,7 +74,9 @@ void parse_block(const std::string& blk, std::vector<std::pair<std::string, std:
     const uint64_t shared = get_varint(p, end);
     const uint64_t nonshared = get_varint(p, end);
     const uint64_t vlen = get_varint(p, end);
-    if (shared > key.size() || nonshared + vlen > uint64_t(end - p)) throw std::runtime_error("sstable: bad entry");
+    const uint64_t avail = uint64_t(end - p);
+    if (shared > key.size() || nonshared > avail || vlen > avail - nonshared)
+      throw std::runtime_error("sstable: bad entry");
     key.resize(shared);
     key.append(reinterpret_cast<const char*>(p), nonshared);
     p += nonshared;

@@ -97,6 +97,7 @@ TensorView parse_tensor(Reader r) {
         t.content_size = size_t(c.end - c.p);
       }
     } else if (f == 5 && w == I32) {           // unpacked float_val
+      if (r.end - r.p < 4) throw ProtoError("truncated fixed32");
       t.values_field = 5;
       t.unpacked.insert(t.unpacked.end(), r.p, r.p + 4);
       r.p += 4;

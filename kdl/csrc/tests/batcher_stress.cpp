@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
         const int64_t t = b.submit(data.data(), n, deadline);
         if (t < 0) { rejected++; continue; }
         std::vector<float> out(n * o.out_cols);
-        const int st = b.wait(t, out.data());
+        const int st = b.wait(t, out.data(), out.size());
         if (st == ST_OK) {
           for (int i = 0; i < n; ++i)
             for (int k = 0; k < o.out_cols; ++k)

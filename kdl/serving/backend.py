@@ -220,6 +220,11 @@ class _Executor(threading.Thread):
                     self.healthy = False
                     log.error("executor %s: %d consecutive failures, marking device unhealthy and leaving "
                               "the batcher to the other devices", self.name, self.failures)
+                    if not self.runner.healthy():
+                        # nobody is left to pull from the queue: fail what is queued (waiters with
+                        # no deadline would otherwise block forever) and refuse new submits
+                        log.error("no healthy executor left for %s: failing queued requests", self.runner.sig.name)
+                        b.shutdown()
                     return
                 continue
             dt = (time.perf_counter() - t0) * 1e3
@@ -368,8 +373,8 @@ class SignatureRunner:
             chunk = mv[s * item_bytes:(s + k) * item_bytes]
             t = self.batcher.submit(chunk, k, deadline_us)
             if t < 0:
-                for _, tt, _ in tickets:   # drain what was already queued
-                    self.batcher.wait(tt, np.empty((1, ncls), np.float32))
+                for ss, tt, _ in tickets:  # drain what was already queued, each into a buffer of its size
+                    self.batcher.wait(tt, np.empty((min(self.max_batch, n - ss), ncls), np.float32))
                 raise ServingError("RESOURCE_EXHAUSTED" if -t == rt.ST_QUEUE_FULL else "UNAVAILABLE",
                                    f"batcher rejected request (status {-t})")
             tickets.append((s, t, chunk))

@@ -60,11 +60,18 @@ def _payload(raw: bytes, td: dict, sig) -> tuple[object, int]:
                 return np.full((n, IMG, IMG, 3), v, dtype=np.float32), n
             raise ServingError("INVALID_ARGUMENT", f"tensor content has {td['size']} bytes, expected {need}")
         return memoryview(raw)[td["offset"]:td["offset"] + need], n
-    if td["unpacked"]:
-        arr = np.frombuffer(td["unpacked"], dtype=np.float32)
-    else:  # typed *_val that needs protobuf decoding (e.g. packed varint int_val for uint8)
-        req = P.PredictRequest.FromString(raw)
-        arr = P.tensor_proto_to_np(req.inputs[td["key"]])
+    try:
+        if td["unpacked"]:
+            arr = np.frombuffer(td["unpacked"], dtype=np.float32)
+        else:  # typed *_val that needs protobuf decoding (e.g. packed varint int_val for uint8)
+            req = P.PredictRequest.FromString(raw)
+            arr = P.tensor_proto_to_np(req.inputs[td["key"]])
+    except (ValueError, KeyError, TypeError) as e:
+        raise ServingError("INVALID_ARGUMENT", f"cannot decode input '{sig.input_key}': {e}") from e
+    if arr.size != n * IMG * IMG * 3:
+        # TF-Serving: "Input to reshape is a tensor with X values, but the requested shape has Y"
+        raise ServingError("INVALID_ARGUMENT", f"input '{sig.input_key}' has {arr.size} values, but its "
+                           f"shape {dims} needs {n * IMG * IMG * 3}")
     arr = np.ascontiguousarray(arr.reshape(n, IMG, IMG, 3),
                                dtype=np.uint8 if sig.input_dtype == P.DT_UINT8 else np.float32)
     return arr, n

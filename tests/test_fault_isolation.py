@@ -72,3 +72,37 @@ def test_not_ready_when_every_device_failed(tmp_path, monkeypatch):
         assert e.value.code() == grpc.StatusCode.UNAVAILABLE
     finally:
         srv.stop(0)
+
+
+def test_no_deadline_requests_fail_when_last_executor_leaves(tmp_path, monkeypatch):
+    """Requests without a deadline (REST without X-Deadline-Ms, gRPC without a timeout)
+    that are queued when the last healthy executor leaves must fail, not block forever."""
+    import threading
+
+    from kdl.serving.backend import ServingError
+    srv = _server(tmp_path, monkeypatch, "fail=cpu:-1,delay=cpu:20")
+    try:
+        runner = srv.manager.get("m").runner("serving_default")
+        x = np.zeros((1, 224, 224, 3), np.uint8)
+        codes, lock = [], threading.Lock()
+
+        def call():
+            try:
+                runner.predict(x, 1, 0)        # deadline 0 = none
+                code = "OK"
+            except ServingError as e:
+                code = e.code
+            with lock:
+                codes.append(code)
+
+        ths = [threading.Thread(target=call, daemon=True) for _ in range(16)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(timeout=60)
+        assert not any(t.is_alive() for t in ths), "a no-deadline request hung after every executor failed"
+        assert len(codes) == 16 and "OK" not in codes
+        assert set(codes) <= {"INTERNAL", "UNAVAILABLE"}
+        assert not runner.healthy()
+    finally:
+        srv.stop(0)

@@ -113,6 +113,18 @@ def test_errors_map_to_grpc_codes(channel):
     with pytest.raises(grpc.RpcError) as e:
         stub.Predict(make_request(x, signature="nope"), timeout=5)
     assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    # typed float_val whose value count does not match the declared shape (neither
+    # the full count nor a single broadcast value) -> INVALID_ARGUMENT, not UNKNOWN
+    bad = P.PredictRequest()
+    bad.model_spec.name = "clothing-model"
+    t = bad.inputs["input_8"]
+    t.dtype = P.DT_FLOAT
+    for d in (1, 299, 299, 3):
+        t.tensor_shape.dim.add(size=d)
+    t.float_val.extend([0.5] * 7)
+    with pytest.raises(grpc.RpcError) as e:
+        stub.Predict(bad, timeout=5)
+    assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
     req = make_request(x)
     req.model_spec.version.value = 42
     with pytest.raises(grpc.RpcError) as e:
