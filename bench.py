@@ -47,13 +47,20 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--model", default="xception",
                     help="xception (headline) | resnet50 | vit_b16 | vit_b16_fp8 | efficientnet_b7")
-    ap.add_argument("--ingress", choices=["scatter", "local"], default="scatter")
+    ap.add_argument("--ingress", choices=["scatter", "local", "none"], default="scatter",
+                    help="none: DIAGNOSTIC ONLY (no host->device copy; the graphs re-read stale "
+                         "slots) to measure what ingress overlap costs; never a reported number")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--depth", type=int, default=2,
+    ap.add_argument("--depth", type=int, default=3,
                     help="ingress prefetch distance in batches (input slots = depth + 1)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="split each GPU's batch into this many concurrent hipGraph lanes "
                          "(kdl/engine/lanes.py; default 2 when the batch is even)")
+    ap.add_argument("--lanes-free", action="store_true",
+                    help="free-running lane streams (LaneGroup.launch_async) instead of forking/joining "
+                         "the lanes through one stream every batch (measured 1-3 %% slower on one GPU)")
+    ap.add_argument("--copy", choices=["raw", "torch"], default="raw",
+                    help="ingress/egress copies: raw hipMemcpyAsync (kdl._C.memcpy_async) or torch copy_")
     ap.add_argument("--no-tune", action="store_true")
     ap.add_argument("--retune", action="store_true", help="autotune even if a tuning table exists")
     ap.add_argument("--tuning", default=None, help="tuning table to load instead of kdl/tuning/<model>_b<batch>.json")
@@ -78,6 +85,8 @@ def main(argv=None) -> int:
             dist.init_process_group(a.dist_backend)
 
     from kdl.engine import registry
+    from kdl.ops import _lib
+    C = _lib.lib()
     from kdl.engine.tuning import tuning_path
 
     B = a.batch
@@ -108,15 +117,18 @@ def main(argv=None) -> int:
     # Ingress is double-buffered: the H2D of batch i+1 runs on a copy stream while
     # batch i computes (what the serving executor does with its pinned staging).
     n_host = n_global if a.ingress == "scatter" else B
-    has_host = a.ingress == "local" or rank == 0
-    host = (torch.randint(0, 256, (n_host, S, S, 3), generator=g, dtype=torch.uint8).pin_memory()
-            if has_host else None)
+    has_host = a.ingress == "local" or (a.ingress == "scatter" and rank == 0)
+    # one pinned host batch per slot (a server's requests land in distinct staging buffers;
+    # re-issuing copies from ONE pinned buffer while its previous copy is still queued
+    # blocked hipMemcpyAsync on the host for ~0.6 ms per step)
+    NS = a.depth + 1
+    hosts = ([torch.randint(0, 256, (n_host, S, S, 3), generator=g, dtype=torch.uint8).pin_memory()
+              for _ in range(NS)] if has_host else None)
     # NS engine slots (input + logits buffer, each with its own captured graph): batch
     # i+depth lands in one slot (H2D, or RCCL scatter) and batch i-1's logits leave
     # another while batch i's graph runs; no device-to-device copies anywhere.
-    NS = a.depth + 1
     slots = eng.add_input_slots(NS)
-    direct = world == 1 or a.ingress == "local"      # H2D straight into the slot
+    direct = world == 1 or a.ingress != "scatter"    # H2D straight into the slot
     stage = ([torch.empty((n_host, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(NS)]
              if has_host and not direct else [None] * NS)
     NC = info.classes
@@ -128,8 +140,12 @@ def main(argv=None) -> int:
     ms = torch.cuda.Stream(device=dev) if world > 1 else None   # RCCL scatter / gather + egress D2H
     ds = torch.cuda.Stream(device=dev) if world == 1 else None  # egress D2H (one GPU)
     E = lambda: [torch.cuda.Event() for _ in range(NS)]  # noqa: E731
-    ready, scattered, free, drained = E(), E(), E(), E()
-    for e in free + drained + scattered:
+    ready, scattered, drained = E(), E(), E()
+    # free[j]: slot j's input and logits are final -- one event per lane (free-running
+    # lanes, LaneGroup.launch_async) or one for the single graph
+    nl = a.lanes if a.lanes > 1 and a.lanes_free else 1
+    free = [[torch.cuda.Event() for _ in range(nl)] for _ in range(NS)]
+    for e in drained + scattered + [f for fs in free for f in fs]:
         e.record(s)
     total = a.warmup + a.steps
     t_in = [torch.cuda.Event(enable_timing=True) for _ in range(total + 1)]
@@ -140,13 +156,25 @@ def main(argv=None) -> int:
     # stream) and batch i-1's logits are gathered (comm) and copied out (egress).
     def ingress(i, timed=False):
         j = i % NS
+        t0 = time.perf_counter()
+        # slot j (and stage j) must no longer be read by the graph / scatter of batch
+        # i-NS. Waited for on the HOST, not with cs.wait_event: an H2D issued behind a
+        # device-side wait on a graph-launch event held the issuing thread until that
+        # graph finished (~0.6 ms per step, the GPU then ran dry between batches). With
+        # depth >= 3 these events completed long ago, so the host waits nothing.
+        for f in free[j]:
+            f.synchronize()
+        scattered[j].synchronize()
         with torch.cuda.stream(cs):
-            cs.wait_event(free[j])          # slot j no longer read by the graph of batch i-NS
-            cs.wait_event(scattered[j])     # stage j no longer read by the scatter of batch i-NS
             if timed:
                 t_in[i].record(cs)
             if has_host:
-                (slots[j][:B] if direct else stage[j]).copy_(host, non_blocking=True)
+                dst, host = (slots[j][:B] if direct else stage[j]), hosts[j]
+                if a.copy == "raw":
+                    C.memcpy_async(dst.data_ptr(), host.data_ptr(), host.numel(), 1, cs.cuda_stream)
+                else:
+                    dst.copy_(host, non_blocking=True)
+            tt[0] += time.perf_counter() - t0
             ready[j].record(cs)
         if not direct:
             with torch.cuda.stream(ms):
@@ -156,11 +184,15 @@ def main(argv=None) -> int:
 
     def compute(i):
         j = i % NS
+        inp = ready[j] if direct else scattered[j]
+        if nl > 1:                          # lanes replay free-running on their own streams
+            eng.launch_async(B, [inp, drained[j]], free[j], capture=use_graph, slot=j)
+            return
         with torch.cuda.stream(s):
-            s.wait_event(ready[j] if direct else scattered[j])
+            s.wait_event(inp)
             s.wait_event(drained[j])        # slot j's logits left (gather + D2H of batch i-NS)
             eng.launch(B, s, capture=use_graph, slot=j)
-            free[j].record(s)               # input and logits of slot j are final
+            free[j][0].record(s)            # input and logits of slot j are final
 
     def collect(i, timed=False):
         j = i % NS
@@ -169,25 +201,44 @@ def main(argv=None) -> int:
             # gather + D2H on the comm stream: one fewer stream, so compute, lanes, H2D
             # and comm each keep a hardware queue of their own (GPU_MAX_HW_QUEUES=4)
             with torch.cuda.stream(ms):
-                ms.wait_event(free[j])
+                for f in free[j]:
+                    ms.wait_event(f)
                 dist.gather(out, list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
                 if rank == 0:
-                    out_host[j].copy_(logits_all[j], non_blocking=True)
+                    d2h(out_host[j], logits_all[j], ms)
                 drained[j].record(ms)
                 if timed:
                     t_out[i].record(ms)
             return
         with torch.cuda.stream(ds):
-            ds.wait_event(free[j])
-            out_host[j].copy_(out, non_blocking=True)
+            for f in free[j]:
+                ds.wait_event(f)
+            d2h(out_host[j], out, ds)
             drained[j].record(ds)
             if timed:
                 t_out[i].record(ds)
 
+    def d2h(dst, src, stream):
+        if a.copy == "raw":
+            n = min(dst.numel(), src.numel()) * src.element_size()
+            C.memcpy_async(dst.data_ptr(), src.data_ptr(), n, 2, stream.cuda_stream)
+        else:
+            dst[:src.shape[0]].copy_(src, non_blocking=True)
+
+    tt = [0.0, 0.0, 0.0]   # host seconds in ingress / compute / collect issue
+
     def step(i):
-        ingress(i + a.depth)  # prefetch `depth` batches ahead (K timed steps = K ingresses + K forwards)
+        # compute first: hipMemcpyAsync of the pinned ingress blocks the host until the
+        # copy stream's event waits resolve (the graph that last read the slot), which
+        # measured ~0.75 ms/step of host time; issued after batch i's graphs, that wait
+        # overlaps a queued graph instead of draining the GPU at every step
+        t1 = time.perf_counter()
         compute(i)
+        t2 = time.perf_counter()
         collect(i)
+        tt[1] += t2 - t1
+        tt[2] += time.perf_counter() - t2
+        ingress(i + a.depth)  # prefetch `depth` batches ahead (K timed steps = K ingresses + K forwards)
 
     # setup (not a warmup step): capture both slots' graphs and let the clocks ramp
     for j in range(NS):
@@ -208,6 +259,7 @@ def main(argv=None) -> int:
         dist.barrier()
     torch.cuda.synchronize()
 
+    tt[:] = [0.0, 0.0, 0.0]
     t0 = time.perf_counter()
     for i in range(a.warmup, total):
         step(i)
@@ -267,7 +319,8 @@ def main(argv=None) -> int:
                        "ingress": a.ingress, "hipgraph": use_graph, "lanes": a.lanes},
         }
         print(json.dumps(res), flush=True)
-        print(f"host issue time {t_issue * 1e3 / a.steps:.3f} ms/step", file=sys.stderr)
+        print(f"host issue time {t_issue * 1e3 / a.steps:.3f} ms/step (ingress {tt[0] * 1e3 / a.steps:.3f}, "
+              f"compute {tt[1] * 1e3 / a.steps:.3f}, collect {tt[2] * 1e3 / a.steps:.3f})", file=sys.stderr)
         if a.profile_layers:
             for name, t in eng.profile(B, 10):
                 print(f"{name:28s} {t * 1e3:9.1f} us", file=sys.stderr)

@@ -193,6 +193,12 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(bm, bn, th);
   });
   m.def("conv_gemm_num_configs", &conv_gemm_num_configs);
+  // raw async copy (kind: hipMemcpyKind, 1 = H2D, 2 = D2H): the pipelined ingress /
+  // egress of bench.py and the serving executor without torch's per-copy bookkeeping
+  m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, int kind, uintptr_t s) {
+    py::gil_scoped_release nogil;
+    chk(hipMemcpyAsync((void*)dst, (const void*)src, n, (hipMemcpyKind)kind, S(s)), "memcpy_async");
+  });
   m.def("sepconv_pipe_fits", &sepconv_pipe_fits);
   m.def("dw3x3", [](py::dict d, uintptr_t s) {
     const auto a = dw_args(d);

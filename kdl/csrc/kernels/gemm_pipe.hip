@@ -26,7 +26,14 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB>
+// ABL: timing-ablation bits (tools/kbench.py --cfgs; never autotune candidates):
+//   1 no MFMA, 2 no LDS-DMA in the k-loop, 4 no global stores, 8 no LDS fragment reads,
+//   16 A fragments DMA'd from a contiguous 1 KiB source (same bytes, B-like full-line
+//   access instead of 16 rows x 64 B; wrong values, timing only), 32 no A DMA,
+//   64 no B DMA, 128 rotate the k order per workgroup (a real variant: workgroups
+//   sharing the weights start at different k-steps instead of all requesting the same
+//   weight fragments at once)
+template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int ABL = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs a) {
   constexpr int NW = WGM * WGN;
   constexpr int BM = 16 * FM * WGM;
@@ -77,11 +84,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   // Issue stage t (k32 steps t*KSUB .. t*KSUB+KSUB-1). A sub-step past the end
   // of K re-issues the stage's first sub-step into its own slot (its MFMAs are
   // skipped), so every stage has exactly L*KSUB DMAs for the counted vmcnt.
+  const int krot = (ABL & 128) ? (int)(blockIdx.x % (unsigned)KT32) : 0;
   auto issue = [&](int t, int buf) {
 #pragma unroll
     for (int ks = 0; ks < KSUB; ++ks) {
       int k32 = t * KSUB + ks;
       if (k32 >= KT32) k32 = t * KSUB;
+      if constexpr ((ABL & 128) != 0) {
+        k32 += krot;
+        k32 = k32 >= KT32 ? k32 - KT32 : k32;
+      }
       long koff_a;
       if constexpr (MODE == 0) {
         koff_a = (long)k32 * 32;
@@ -94,8 +106,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
 #pragma unroll
       for (int i = 0; i < L; ++i) {
         const int f = min(wave + i * NW, FR - 1);
-        if (f < AF) glds16(a.x + src[i] + koff_a, base + f * 1024);
-        else glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
+        if (f < AF) {
+          if constexpr (ABL & 32) {
+          } else if constexpr (ABL & 16)
+            glds16(a.x + ((long)min(m0 / 16 + f, a.M / 16 - 1) * KT32 + k32) * 512 + lane * 8, base + f * 1024);
+          else
+            glds16(a.x + src[i] + koff_a, base + f * 1024);
+        }
+        else if constexpr (!(ABL & 64)) glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
       }
     }
   };
@@ -116,24 +134,38 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     if (after >= 2) wait_vm_barrier<2 * L * KSUB>();
     else if (after == 1) wait_vm_barrier<L * KSUB>();
     else wait_vm_barrier<0>();
-    if (t + STAGES - 1 < KT) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    if (!(ABL & 2) && t + STAGES - 1 < KT) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
 #pragma unroll
     for (int ks = 0; ks < KSUB; ++ks) {
       if (KSUB > 1 && t * KSUB + ks >= KT32) break;
       const uint8_t* st = smem + (t % STAGES) * STAGE + ks * FR * 1024 + lane * 16;
       s16x8 af[FM], bf[FN];
+      if constexpr (ABL & 8) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
+        for (int i = 0; i < FM; ++i) af[i] = (s16x8){(short)(t + i), 1, 2, 3, 4, 5, 6, (short)lane};
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
+        for (int j = 0; j < FN; ++j) bf[j] = (s16x8){(short)(t + j), 3, 2, 1, 4, 5, 6, (short)ks};
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
+      }
       // raise this wave's issue priority while it streams MFMAs (guide §5 T-setprio:
       // the other waves' glds issue / barrier arrival no longer interleave into the
       // MFMA run)
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (ABL & 1) {
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+          for (int j = 0; j < FN; ++j) acc[i][j][0] += __uint_as_float((uint32_t)af[i][0] ^ (uint32_t)bf[j][1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+      }
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -162,7 +194,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
     if (m < a.M && n < a.nstore) {
-      epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+      if constexpr (ABL & 4) {
+        if (smem[r * CS + cc * 16] == 0x7f && smem[r * CS + cc * 16 + 1] == 0x7f) a.y[0] = 1;   // keep the tile live
+      } else {
+        epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+      }
     }
   }
 }
@@ -197,12 +233,33 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   X(25, 4, 2, 2, 4, 6, 1)   \
   X(26, 6, 3, 2, 4, 3, 2)
 
-template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS>
+// timing ablations of id 9 (ABL bits above), ids 27..44
+#define KDL_PIPE_ABL(X) \
+  X(27, 6, 3, 2, 4, 3, 1, 1) \
+  X(28, 6, 3, 2, 4, 3, 1, 2) \
+  X(29, 6, 3, 2, 4, 3, 1, 4) \
+  X(30, 6, 3, 2, 4, 3, 1, 8) \
+  X(31, 6, 3, 2, 4, 3, 1, 15) \
+  X(32, 6, 3, 2, 4, 3, 1, 16) \
+  X(33, 6, 3, 2, 4, 3, 1, 20) \
+  X(34, 6, 3, 2, 4, 3, 1, 13) \
+  X(35, 6, 3, 2, 4, 5, 1, 13) \
+  X(36, 6, 3, 2, 4, 5, 1, 0)  \
+  X(37, 6, 3, 2, 4, 2, 2, 13) \
+  X(38, 6, 3, 2, 4, 2, 2, 0)  \
+  X(39, 6, 3, 2, 4, 3, 2, 13) \
+  X(40, 6, 3, 2, 4, 3, 2, 0)  \
+  X(41, 6, 3, 2, 4, 3, 1, 45) \
+  X(42, 6, 3, 2, 4, 3, 1, 77) \
+  X(43, 6, 3, 2, 4, 3, 1, 141) \
+  X(44, 6, 3, 2, 4, 3, 1, 128)
+
+template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int ABL = 0>
 static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
   const int nM = (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS>), dim3(nM * nN), dim3(64 * WGM * WGN), 0,
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, ABL>), dim3(nM * nN), dim3(64 * WGM * WGN), 0,
                      s, a);
   return hipGetLastError();
 }
@@ -214,6 +271,10 @@ static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s
   case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks>(a, s);
     KDL_PIPE_CONFIGS(KDL_PCASE)
 #undef KDL_PCASE
+#define KDL_PACASE(id, fm, fn, wgm, wgn, st, ks, abl) \
+  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, abl>(a, s);
+    KDL_PIPE_ABL(KDL_PACASE)
+#undef KDL_PACASE
     default: return hipErrorInvalidValue;
   }
 }
@@ -221,7 +282,7 @@ static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (a.K % 32 != 0 || a.M <= 0) return hipErrorInvalidValue;
   if (mode == 0) return launch_pipe_mode<0>(cfg, a, s);
-  if (mode == 1) return launch_pipe_mode<1>(cfg, a, s);
+  if (mode == 1 && cfg < 27) return launch_pipe_mode<1>(cfg, a, s);
   return hipErrorInvalidValue;
 }
 
@@ -231,6 +292,10 @@ int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads) {
   case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
     KDL_PIPE_CONFIGS(KDL_PINFO)
 #undef KDL_PINFO
+#define KDL_PAINFO(id, fm, fn, wgm, wgn, st, ks, abl) \
+  case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
+    KDL_PIPE_ABL(KDL_PAINFO)
+#undef KDL_PAINFO
     default: return -1;
   }
 }

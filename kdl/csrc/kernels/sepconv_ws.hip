@@ -112,6 +112,11 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
       long p = P0 + slot;
       p = p < 0 ? 0 : (p >= NPIX ? NPIX - 1 : p);
       xsrc[i] = slot < NS ? (const uint8_t*)(a.x + p * a.ldx + q * 8) : sepw_zeros;
+      if constexpr (ABL & 16) {                  // timing ablation: 16 pixels x 64 B per instruction
+        long pr = P0 + min(wn + 4 * i, XB - 1) * 16 + (lane >> 2);
+        pr = pr < 0 ? 0 : (pr >= NPIX ? NPIX - 1 : pr);
+        xsrc[i] = (const uint8_t*)(a.x + pr * a.ldx + (lane & 3) * 8);
+      }
     }
     // stages past the end (the branch-free loop keeps issuing) re-load the last one (a scalar
     // clamp; a per-lane select to a zero block cost more VALU than the drain it saves)
@@ -329,7 +334,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
 
 // (FM, FN, STAGES, XB = band KiB): tile BM = 16*FM, BN = 64*FN; LDS = STAGES*(XB+1) KiB + 2FM KiB
 // (+ the BM x BN bf16 C tile, which reuses it); the band needs BM + 2W + 3 <= 16*XB.
-// ids 7..: s_memtime stamping variants with timing ablations (tools/stamps.py; never tuned).
+// ids 7..14: s_memtime stamping variants with timing ablations (tools/stamps.py; never tuned).
 #define KDL_SEPW_CONFIGS(X) \
   X(0, 6, 6, 5, 9)          \
   X(1, 6, 6, 6, 9)          \
@@ -345,12 +350,20 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(11, 6, 6, 6, 9)         \
   X(12, 6, 6, 6, 9)         \
   X(13, 6, 6, 6, 9)         \
-  X(14, 6, 6, 6, 9)
+  X(14, 6, 6, 6, 9)          \
+  X(15, 12, 3, 5, 15)        \
+  X(16, 8, 3, 5, 11)         \
+  X(17, 12, 3, 6, 15)        \
+  X(18, 6, 6, 5, 9)          \
+  X(19, 4, 6, 5, 8)
 
 // timing-ablation bits of the stamping ids: 1 no depthwise MFMA, 2 no pointwise MFMA,
-// 4 no band / weight LDS-DMA in the loop, 8 producers skip the depthwise entirely
+// 4 no band / weight LDS-DMA in the loop, 8 producers skip the depthwise entirely;
+// ids 18/19 (no stamps): 16 = band DMA'd as 16 pixels x 64 B per instruction (wrong LDS
+// placement for the producers: timing only)
 constexpr int sepw_abl(int id) {
-  return id == 8 ? 1 : id == 9 ? 2 : id == 10 ? 3 : id == 11 ? 4 : id == 12 ? 5 : id == 13 ? 8 : id == 14 ? 12 : 0;
+  return id == 8 ? 1 : id == 9 ? 2 : id == 10 ? 3 : id == 11 ? 4 : id == 12 ? 5 : id == 13 ? 8 : id == 14 ? 12
+       : id == 18 || id == 19 ? 16 : 0;
 }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }
@@ -377,6 +390,9 @@ int sepconv_ws_fits(int cfg, int W) {
 
 hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   int bm, bn, th;
+  // ids 9 / 10 (ablation bit 2, no pointwise MFMA) faulted the GPU once in round 2 (cause not
+  // found); refused until understood -- they are timing ablations, never candidates
+  if (cfg == 9 || cfg == 10) return hipErrorInvalidValue;
   if (sepconv_ws_config(cfg, &bm, &bn, &th) != 0 || !sepconv_ws_fits(cfg, a.W) || a.K % 32 != 0 ||
       a.K > 8192 || (a.NF * 16) % bn != 0 || a.OH != a.H || a.OW != a.W || a.M <= 0 || a.dwk == nullptr)
     return hipErrorInvalidValue;
@@ -385,10 +401,10 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 #define KDL_SWCASE(id, fm, fn, st, xb)                                                                \
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, (id >= 7), sepw_abl(id), true>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, (id >= 7 && id <= 14), sepw_abl(id), true>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     else                                                                                            \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, (id >= 7), sepw_abl(id), false>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, (id >= 7 && id <= 14), sepw_abl(id), false>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)

@@ -1,0 +1,143 @@
+"""Whole-graph tile tuning: coordinate descent on the replay time of the captured
+forward (all lanes running), instead of timing each layer alone.
+
+Why: the per-layer autotuner (``EngineBase.autotune``) times a layer's variants
+in isolation on an idle chip. In the real step, two lanes replay concurrently
+(``lanes.py``) and every kernel shares the chip with the other lane's current
+layer, so the solo-fastest tile is only a proxy. Measured on MI355X: at 16
+images per lane the middle-flow fused separable conv is 18 % faster alone with
+the 64-row tile than with the 96-row tile the b32 table uses, but the 64-row
+tile launches 50 % more workgroups, which is exactly what the other lane then
+competes with. Only the graph time settles it.
+
+Procedure: start from the committed table; for each tunable layer in graph
+order, try every valid (split, cfg) variant on all lanes at once, re-capture the
+hipGraphs and time ``reps`` replays of the full forward; a challenger replaces
+the incumbent only if it wins an interleaved A/B re-measurement (``confirm``
+rounds, median) by more than ``margin``. One pass is ~N_variants graph captures.
+
+    python -m kdl.engine.graph_tune --model xception --batch 32 --lanes 2 \
+        --out kdl/tuning/xception_b32_l2.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+
+def _steps_of(eng):
+    return eng.engines[0].conv_steps() if hasattr(eng, "engines") else eng.conv_steps()
+
+
+def _variants_of(eng, step):
+    e0 = eng.engines[0] if hasattr(eng, "engines") else eng
+    return e0._variants(step)
+
+
+def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
+    """ms per forward replay (all lanes), after (re)capturing the graphs."""
+    s = eng.stream
+    eng.launch(b, s, capture=True)            # builds + captures any invalidated program
+    for _ in range(warm):
+        eng.launch(b, s, capture=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        eng.launch(b, s, capture=True)
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, margin: float = 0.002,
+               log=print) -> dict:
+    table = dict(eng.tuning())
+    eng.apply_tuning(table)
+    base = statistics.median(graph_time(eng, b, reps) for _ in range(3))
+    log(f"start: {base * 1e3:.1f} us/forward")
+    t_start = base
+    for p in range(passes):
+        changed = 0
+        steps = _steps_of(eng)
+        for i, step in enumerate(steps):
+            name = step.name
+            cur = table[name]
+            log(f"  [{i + 1}/{len(steps)}] {name} ({len(_variants_of(eng, step))} variants) at {base * 1e3:.1f} us")
+            for split, cfg in _variants_of(eng, step):
+                cand = [int(split), int(cfg)]
+                if cand == cur:
+                    continue
+                trial = dict(table, **{name: cand})
+                eng.apply_tuning(trial)
+                t = graph_time(eng, b, reps)
+                if t >= base * (1 - margin):
+                    continue
+                # interleaved A/B: incumbent vs challenger, median of `confirm` rounds each
+                ta, tb = [], []
+                for _ in range(confirm):
+                    eng.apply_tuning(table)
+                    ta.append(graph_time(eng, b, reps))
+                    eng.apply_tuning(trial)
+                    tb.append(graph_time(eng, b, reps))
+                ma, mb = statistics.median(ta), statistics.median(tb)
+                if mb < ma * (1 - margin):
+                    log(f"  {name:22s} {cur} -> {cand}: {ma * 1e3:8.1f} -> {mb * 1e3:8.1f} us")
+                    table, base, cur = trial, mb, cand
+                    changed += 1
+                else:
+                    base = ma
+            eng.apply_tuning(table)
+        log(f"pass {p}: {changed} change(s), {base * 1e3:.1f} us/forward")
+        if not changed:
+            break
+    eng.apply_tuning(table)
+    log(f"graph tune: {t_start * 1e3:.1f} -> {base * 1e3:.1f} us/forward")
+    return table
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="xception")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--lanes", type=int, default=2)
+    ap.add_argument("--passes", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--start", default=None, help="starting table (default: the committed table)")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args(argv)
+    from . import registry
+    from .tuning import tuning_path
+    dev = torch.device("cuda", 0)
+    info = registry.get(a.model)
+    params = info.init_params(0)
+    if a.lanes > 1:
+        from .lanes import LaneGroup
+        eng = LaneGroup(info, params, a.batch, dev, a.lanes)
+    else:
+        eng = info.engine(params, a.batch, dev)
+    start = Path(a.start) if a.start else tuning_path(a.model, a.batch, a.lanes)
+    if not start.exists():
+        start = tuning_path(a.model, a.batch)
+    eng.load_tuning(start)
+    # random input (DVFS / MFMA clock behaviour differs on zeros)
+    g = torch.Generator().manual_seed(0)
+    inp = eng.inp
+    if inp.dtype == torch.uint8:
+        inp.copy_(torch.randint(0, 256, tuple(inp.shape), generator=g, dtype=torch.uint8))
+    else:
+        inp.copy_(torch.rand(tuple(inp.shape), generator=g) * 2 - 1)
+    t0 = time.time()
+    table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True))
+    Path(a.out).write_text(json.dumps(table, indent=1))
+    print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

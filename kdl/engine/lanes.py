@@ -163,6 +163,22 @@ class LaneGroup:
         for k in range(1, self.lanes):
             s.wait_event(self._join[k])
 
+    def launch_async(self, b: int, wait: list, done: list, capture: bool = True, slot: int = 0) -> None:
+        """Free-running lanes: lane k's stream waits only on ``wait`` (e.g. this
+        slot's ingress and egress events), replays its graph and records ``done[k]``.
+        Unlike ``launch`` there is no fork from / join into one stream, so lane k of
+        batch i+1 starts as soon as lane k of batch i is done instead of waiting for
+        the slowest lane. Measured 1-3 % SLOWER than the joined lanes in bench.py
+        (``--lanes-free``, profiles/ingress_hostsync_ab.txt): lanes that stay
+        layer-aligned share the chip better than lanes that drift, so this is an
+        option, not the default."""
+        assert b == self.max_batch and len(done) == self.lanes, "lanes run full batches only"
+        for e, d in zip(self.engines, done):
+            for w in wait:
+                e.stream.wait_event(w)
+            e.launch(self.b, e.stream, capture, slot)
+            d.record(e.stream)
+
     @torch.no_grad()
     def forward(self, x: torch.Tensor, capture: bool = True) -> torch.Tensor:
         n = x.shape[0]
