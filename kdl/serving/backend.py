@@ -200,38 +200,76 @@ class _Executor(threading.Thread):
         METRICS.gauge("kdl_executor_healthy", lambda: float(self.healthy), executor=self.name)
         b = self.runner.batcher
         rt = _lib.rt()
+        # pipelined executors (GPU, depth >= 2): batch n+1 is pulled into the next pinned
+        # staging slot (host copy of the payloads) and its H2D + graph are issued while
+        # batch n still runs on the device; batch n is finished (results scattered to
+        # the waiting handlers) once its completion event has fired
+        depth = max(1, getattr(self, "depth", 1))
+        pending = []                           # (batch, handle, t0) in issue order
+        slot = 0
         while not self.stop.is_set():
-            batch = b.next_batch(self.staging_ptr(), 100_000)
-            if batch is None:
-                continue
-            t0 = time.perf_counter()
-            METRICS.observe("kdl_stage_ms", (rt.now_us() - batch.oldest_enqueue_us) / 1e3, stage="queue_wait")
-            try:
-                self.faults.before_batch(self.name)
-                out_ptr = self.execute(batch.bucket, batch.n_real)
-                b.finish(batch, out_ptr, rt.ST_OK)
+            poll = 0 if pending else 100_000   # with work in flight, never sleep in the batcher
+            batch = b.next_batch(self.staging_ptr(slot), poll)
+            if batch is not None:
+                t0 = time.perf_counter()
+                METRICS.observe("kdl_stage_ms", (rt.now_us() - batch.oldest_enqueue_us) / 1e3, stage="queue_wait")
+                try:
+                    self.faults.before_batch(self.name)
+                    handle = self.issue(batch.bucket, batch.n_real, slot)
+                except BaseException:  # noqa: BLE001 - fail the batch, keep serving
+                    if self._failed(b, batch):
+                        return
+                    continue
+                pending.append((batch, handle, t0))
+                slot = (slot + 1) % depth
+            if pending and (batch is None or len(pending) >= depth):
+                done, handle, t0 = pending.pop(0)
+                try:
+                    out_ptr = self.complete(handle)
+                except BaseException:  # noqa: BLE001
+                    if self._failed(b, done):
+                        for rest, _, _ in pending:   # leaving: fail what is still in flight
+                            b.finish(rest, 0, rt.ST_ERROR)
+                        return
+                    continue
+                b.finish(done, out_ptr, rt.ST_OK)
                 self.failures = 0
-            except BaseException:  # noqa: BLE001 - fail the batch, keep serving
-                log.exception("batch %d failed on %s", batch.id, self.name)
-                b.finish(batch, 0, rt.ST_ERROR)
-                METRICS.inc("kdl_batch_errors_total", executor=self.name)
-                self.failures += 1
-                if self.failures >= self.max_failures:
-                    self.healthy = False
-                    log.error("executor %s: %d consecutive failures, marking device unhealthy and leaving "
-                              "the batcher to the other devices", self.name, self.failures)
-                    if not self.runner.healthy():
-                        # nobody is left to pull from the queue: fail what is queued (waiters with
-                        # no deadline would otherwise block forever) and refuse new submits
-                        log.error("no healthy executor left for %s: failing queued requests", self.runner.sig.name)
-                        b.shutdown()
-                    return
-                continue
-            dt = (time.perf_counter() - t0) * 1e3
-            METRICS.observe("kdl_batch_exec_ms", dt, executor=self.name)
-            METRICS.observe("kdl_batch_size", batch.n_real, buckets=BATCH_BUCKETS, signature=self.runner.sig.name)
-            METRICS.inc("kdl_batches_total", signature=self.runner.sig.name)
-            METRICS.inc("kdl_padded_items_total", batch.bucket - batch.n_real, signature=self.runner.sig.name)
+                self._observe(done, t0)
+        for rest, _, _ in pending:
+            b.finish(rest, 0, rt.ST_SHUTDOWN)
+
+    def _failed(self, b, batch) -> bool:
+        """Fail one batch; True when this executor gives up its device."""
+        rt = _lib.rt()
+        log.exception("batch %d failed on %s", batch.id, self.name)
+        b.finish(batch, 0, rt.ST_ERROR)
+        METRICS.inc("kdl_batch_errors_total", executor=self.name)
+        self.failures += 1
+        if self.failures < self.max_failures:
+            return False
+        self.healthy = False
+        log.error("executor %s: %d consecutive failures, marking device unhealthy and leaving "
+                  "the batcher to the other devices", self.name, self.failures)
+        if not self.runner.healthy():
+            # nobody is left to pull from the queue: fail what is queued (waiters with
+            # no deadline would otherwise block forever) and refuse new submits
+            log.error("no healthy executor left for %s: failing queued requests", self.runner.sig.name)
+            b.shutdown()
+        return True
+
+    def _observe(self, batch, t0: float) -> None:
+        dt = (time.perf_counter() - t0) * 1e3
+        METRICS.observe("kdl_batch_exec_ms", dt, executor=self.name)
+        METRICS.observe("kdl_batch_size", batch.n_real, buckets=BATCH_BUCKETS, signature=self.runner.sig.name)
+        METRICS.inc("kdl_batches_total", signature=self.runner.sig.name)
+        METRICS.inc("kdl_padded_items_total", batch.bucket - batch.n_real, signature=self.runner.sig.name)
+
+    # synchronous executors implement execute(); pipelined ones override issue/complete
+    def issue(self, bucket: int, n_real: int, slot: int):
+        return self.execute(bucket, n_real)
+
+    def complete(self, handle) -> int:
+        return handle
 
 
 class GPUExecutor(_Executor):
@@ -273,26 +311,57 @@ class GPUExecutor(_Executor):
                 self.lanes.load_tuning(tp)
             self.lanes.program(bs[-1], capture=True)
             self.lanes.launch(bs[-1])
+        # pipelining depth (batches in flight per GPU): staging / output slots, each with
+        # its own captured graphs (engine input slots), so the host can form batch n+1
+        # while batch n runs
+        self.depth = max(1, int(self.engine_kwargs.get("depth", os.environ.get("KDL_EXEC_DEPTH", "2"))))
+        for e in (self.engine, self.lanes):
+            if e is not None:
+                e.add_input_slots(self.depth)
         dt = torch.uint8 if in_kind == "u8" else torch.float32
         S = src.input_size
-        self.staging = torch.zeros((bs[-1], S, S, 3), dtype=dt).pin_memory()
-        self.out = torch.zeros((bs[-1], src.classes), dtype=torch.float32).pin_memory()
-        for bk in bs:                         # warm-up + capture one hipGraph per bucket
-            self.engine.program(bk, capture=True)
-            self.engine.launch(bk)
+        self.staging = [torch.zeros((bs[-1], S, S, 3), dtype=dt).pin_memory() for _ in range(self.depth)]
+        self.out = [torch.zeros((bs[-1], src.classes), dtype=torch.float32).pin_memory()
+                    for _ in range(self.depth)]
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self.h2d_done = [torch.cuda.Event() for _ in range(self.depth)]
+        self.done = [torch.cuda.Event() for _ in range(self.depth)]
+        self._rt = _lib.lib()
+        for slot in range(self.depth):        # warm-up + capture one hipGraph per (bucket, slot)
+            for bk in bs:
+                self.engine.program(bk, capture=True, slot=slot)
+                self.engine.launch(bk, slot=slot)
+            if self.lanes is not None:
+                self.lanes.program(bs[-1], capture=True, slot=slot)
+                self.lanes.launch(bs[-1], slot=slot)
         torch.cuda.synchronize(self.device)
 
-    def staging_ptr(self) -> int:
-        return self.staging.data_ptr()
+    def staging_ptr(self, slot: int = 0) -> int:
+        return self.staging[slot].data_ptr()
+
+    def issue(self, bucket: int, n_real: int, slot: int) -> int:
+        """H2D on the copy stream (no device-side wait on a graph event: the slot's
+        previous batch was completed on the host before the batcher refilled it),
+        then the bucket's graph and the logits D2H on the engine stream."""
+        e = self.lanes if self.lanes is not None and bucket == self.lanes.max_batch else self.engine
+        C = self._rt
+        stg, inp = self.staging[slot], e.inputs[slot]
+        nbytes = bucket * stg[0].numel() * stg.element_size()
+        C.memcpy_async(inp.data_ptr(), stg.data_ptr(), nbytes, 1, self.copy_stream.cuda_stream)
+        self.h2d_done[slot].record(self.copy_stream)
+        e.stream.wait_event(self.h2d_done[slot])
+        e.launch(bucket, e.stream, slot=slot)
+        lg = e.slot_logits(slot)
+        C.memcpy_async(self.out[slot].data_ptr(), lg.data_ptr(), bucket * lg.shape[1] * 4, 2, e.stream.cuda_stream)
+        self.done[slot].record(e.stream)
+        return slot
+
+    def complete(self, slot: int) -> int:
+        self.done[slot].synchronize()
+        return self.out[slot].data_ptr()
 
     def execute(self, bucket: int, n_real: int) -> int:
-        e = self.lanes if self.lanes is not None and bucket == self.lanes.max_batch else self.engine
-        with torch.cuda.stream(e.stream):
-            e.inp[:bucket].copy_(self.staging[:bucket], non_blocking=True)
-            e.launch(bucket, e.stream)
-            self.out[:bucket].copy_(e.logits[:bucket], non_blocking=True)
-        e.stream.synchronize()
-        return self.out.data_ptr()
+        return self.complete(self.issue(bucket, n_real, 0))
 
 
 class CPUExecutor(_Executor):
@@ -311,7 +380,7 @@ class CPUExecutor(_Executor):
             from ..engine import registry
             self.oracle = registry.get(src.family).oracle
 
-    def staging_ptr(self) -> int:
+    def staging_ptr(self, slot: int = 0) -> int:
         return self.staging.data_ptr()
 
     def execute(self, bucket: int, n_real: int) -> int:

@@ -22,6 +22,32 @@ import grpc  # noqa: E402
 import numpy as np  # noqa: E402
 
 
+def _client_proc(conn, threads: int, req: bytes, seconds: float, warm_s: float) -> None:
+    """Client worker process (spawned BEFORE the server initialises the GPU): receives
+    the target, runs `threads` closed-loop clients, sends back the post-warm-up latencies."""
+    target = conn.recv()
+    lat, lock = [], threading.Lock()
+    t_start = time.perf_counter()
+    stop, warm = t_start + seconds, t_start + warm_s
+
+    def client():
+        ch = grpc.insecure_channel(target, options=[("grpc.max_send_message_length", -1)])
+        call = ch.unary_unary("/tensorflow.serving.PredictionService/Predict")
+        while time.perf_counter() < stop:
+            t0 = time.perf_counter()
+            call(req, timeout=30)
+            t1 = time.perf_counter()
+            if t0 > warm:
+                with lock:
+                    lat.append(t1 - t0)
+    ths = [threading.Thread(target=client) for _ in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    conn.send(lat)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--target", default=None)
@@ -33,7 +59,29 @@ def main(argv=None) -> int:
     ap.add_argument("--max-batch", type=int, default=32)
     ap.add_argument("--timeout-us", type=int, default=1000)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--client-procs", type=int, default=0,
+                    help="run the clients in this many spawned processes (0: threads of the server "
+                         "process, which then share its GIL with the server's handlers)")
     a = ap.parse_args(argv)
+    rng = np.random.default_rng(0)
+    u8 = rng.integers(0, 256, (a.images, 299, 299, 3), dtype=np.uint8)
+    procs = []
+    if a.client_procs:
+        import multiprocessing as mp
+        from kdl.gateway.client import make_request as _mk
+        if a.signature == "serving_uint8":
+            req0 = _mk(u8, signature="serving_uint8", input_key="images").SerializeToString()
+        else:
+            req0 = _mk(u8.astype(np.float32) / 127.5 - 1).SerializeToString()
+        ctx = mp.get_context("spawn")         # before any GPU initialisation in this process
+        per = [a.clients // a.client_procs + (1 if i < a.clients % a.client_procs else 0)
+               for i in range(a.client_procs)]
+        for n in per:
+            parent, child = ctx.Pipe()
+            pr = ctx.Process(target=_client_proc, args=(child, n, req0, a.seconds, min(3.0, a.seconds / 4)),
+                             daemon=True)
+            pr.start()
+            procs.append((pr, parent))
     from kdl.gateway.client import PredictionStub, make_request
     srv = None
     target = a.target
@@ -54,8 +102,6 @@ def main(argv=None) -> int:
         if a.signature != "serving_default":
             srv.manager.get("clothing-model").runner(a.signature)
         target = f"127.0.0.1:{srv.grpc_port}"
-    rng = np.random.default_rng(0)
-    u8 = rng.integers(0, 256, (a.images, 299, 299, 3), dtype=np.uint8)
     if a.signature == "serving_uint8":
         req = make_request(u8, signature="serving_uint8", input_key="images").SerializeToString()
     else:
@@ -63,6 +109,12 @@ def main(argv=None) -> int:
     lat, lock = [], threading.Lock()
     stop = time.perf_counter() + a.seconds
     warm = time.perf_counter() + min(3.0, a.seconds / 4)
+    if procs:
+        for _, conn in procs:
+            conn.send(target)
+        for pr, conn in procs:
+            lat.extend(conn.recv())
+            pr.join()
 
     def client():
         ch = grpc.insecure_channel(target, options=[("grpc.max_send_message_length", -1)])
@@ -74,13 +126,14 @@ def main(argv=None) -> int:
             if t0 > warm:
                 with lock:
                     lat.append(t1 - t0)
-    ths = [threading.Thread(target=client) for _ in range(a.clients)]
+    ths = [threading.Thread(target=client) for _ in range(0 if procs else a.clients)]
     for t in ths:
         t.start()
     for t in ths:
         t.join()
     span = stop - warm
-    res = {"metric": "closed-loop gRPC serving", "clients": a.clients, "images_per_request": a.images,
+    res = {"metric": "closed-loop gRPC serving", "clients": a.clients, "client_procs": a.client_procs,
+           "images_per_request": a.images,
            "signature": a.signature, "requests": len(lat), "images_per_s": round(len(lat) * a.images / span, 1),
            "p50_ms": round(statistics.median(lat) * 1e3, 2),
            "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2)}
