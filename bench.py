@@ -100,9 +100,10 @@ def main(argv=None) -> int:
         eng = LaneGroup(info, params, B, dev, a.lanes)
     else:
         eng = info.engine(params, B, dev)
-    tp = Path(a.tuning) if a.tuning else tuning_path(a.model, B, a.lanes)
+    tname = info.tuning or a.model
+    tp = Path(a.tuning) if a.tuning else tuning_path(tname, B, a.lanes)
     if not a.tuning and not tp.exists():
-        tp = tuning_path(a.model, B)        # no lanes-tuned table: the single-lane one
+        tp = tuning_path(tname, B)          # no lanes-tuned table: the single-lane one
     if tp.exists() and not a.retune:
         eng.load_tuning(tp)
     elif not a.no_tune:
@@ -311,7 +312,7 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": (None if BASELINE_IMG_S is None or a.model != "xception"
                             else round(img_s / BASELINE_IMG_S, 3)),
-            "dtype": "fp8-e4m3 linears / bf16 rest" if a.model.endswith("_fp8") else "bf16",
+            "dtype": info.dtype,
             "data": f"synthetic uint8 {S}x{S}x3 images, random-init weights",
             "config": {"model": info.description,
                        "global_batch": n_global, "seq_len": None, "image_size": S,

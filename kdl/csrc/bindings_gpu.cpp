@@ -40,6 +40,7 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.K = I(d, "K"); a.cin = I(d, "cin", 32); a.NF = I(d, "NF");
   a.nstore = I(d, "nstore"); a.stride = I(d, "stride", 1);
   a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out"); a.opad = I(d, "opad");
+  a.dt = I(d, "dt");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {
@@ -54,7 +55,7 @@ StemArgs stem_args(const py::dict& d) {
   a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.ldy = I(d, "ldy"); a.in_kind = I(d, "in_kind");
   // defaults = the Xception stem (3x3 s2 'valid' -> 32, normalisation folded into the weights)
   a.KH = I(d, "KH", 3); a.KW = I(d, "KW", 3); a.stride = I(d, "stride", 2); a.pad = I(d, "pad", 0);
-  a.cout = I(d, "cout", 32); a.relu = I(d, "relu", 1);
+  a.cout = I(d, "cout", 32); a.relu = I(d, "relu", 1); a.dt = I(d, "dt");
   const char* sk[3] = {"scale0", "scale1", "scale2"};
   const char* hk[3] = {"shift0", "shift1", "shift2"};
   for (int c = 0; c < 3; ++c) { a.scale[c] = F(d, sk[c], 1.f); a.shift[c] = F(d, hk[c], 0.f); }
@@ -63,7 +64,7 @@ StemArgs stem_args(const py::dict& d) {
 GapArgs gap_args(const py::dict& d) {
   GapArgs a{};
   a.x = P<const uint16_t>(d, "x"); a.y = P<float>(d, "y"); a.yb = P<uint16_t>(d, "yb");
-  a.B = I(d, "B"); a.HW = I(d, "HW"); a.ldx = I(d, "ldx"); a.F = I(d, "F");
+  a.B = I(d, "B"); a.HW = I(d, "HW"); a.ldx = I(d, "ldx"); a.F = I(d, "F"); a.dt = I(d, "dt");
   return a;
 }
 FcArgs fc_args(const py::dict& d) {
@@ -140,13 +141,14 @@ FcMfmaArgs fcm_args(const py::dict& d) {
   a.xb = P<const uint16_t>(d, "xb"); a.wp = P<const uint16_t>(d, "wp"); a.bias = P<const float>(d, "bias");
   a.out = P<float>(d, "out");
   a.B = I(d, "B"); a.F = I(d, "F"); a.N = I(d, "N"); a.NF = I(d, "NF"); a.relu = I(d, "relu");
+  a.dt = I(d, "dt");
   return a;
 }
 PoolAddArgs pool_args(const py::dict& d) {
   PoolAddArgs a{};
   a.x = P<const uint16_t>(d, "x"); a.res = P<const uint16_t>(d, "res"); a.y = P<uint16_t>(d, "y");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
-  a.C = I(d, "C"); a.pad_top = I(d, "pad_top"); a.pad_left = I(d, "pad_left");
+  a.C = I(d, "C"); a.pad_top = I(d, "pad_top"); a.pad_left = I(d, "pad_left"); a.dt = I(d, "dt");
   return a;
 }
 HeadArgs head_args(const py::dict& d) {

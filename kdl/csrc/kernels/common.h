@@ -62,6 +62,42 @@ __device__ __forceinline__ void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void*)lds, 16, 0, 0);
 }
 
+// 16-bit activation / weight element type of a kernel instance (DT template parameter,
+// runtime field `dt` in the launch args): 0 = bf16 (every model family's default),
+// 1 = IEEE fp16 (BASELINE.json's "ResNet-50 fp16" config). Both are 16-bit patterns in
+// memory; they differ in the MFMA opcode (v_mfma_f32_16x16x32_{bf16,f16}, same rate on
+// gfx950) and in the fp32 <-> 16-bit conversions. The sign bit is bit 15 in both, so
+// relu_bf16x2 (signed 16-bit max against 0) is exact for fp16 too.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+template <int DT>
+struct Elt;
+
+template <>
+struct Elt<0> {
+  static __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) { return mfma16(a, b, c); }
+  static __device__ __forceinline__ uint32_t pack(float lo, float hi) { return pack_bf16(lo, hi); }
+  static __device__ __forceinline__ float lo(uint32_t d) { return bf_lo(d); }
+  static __device__ __forceinline__ float hi(uint32_t d) { return bf_hi(d); }
+  static __device__ __forceinline__ uint16_t from_f32(float x) { return f2bf(x); }
+};
+
+template <>
+struct Elt<1> {
+  static __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                   0, 0, 0);
+  }
+  static __device__ __forceinline__ uint32_t pack(float lo, float hi) {   // round to nearest even
+    f16x2 v = {(_Float16)lo, (_Float16)hi};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+  static __device__ __forceinline__ float lo(uint32_t d) { return (float)__builtin_bit_cast(f16x2, d)[0]; }
+  static __device__ __forceinline__ float hi(uint32_t d) { return (float)__builtin_bit_cast(f16x2, d)[1]; }
+  static __device__ __forceinline__ uint16_t from_f32(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
+};
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): blocks b, b+8, ... are dispatched to one XCD, so give each XCD a
 // contiguous run of logical tiles; neighbouring tiles then share an L2.

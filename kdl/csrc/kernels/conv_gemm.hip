@@ -37,8 +37,11 @@ namespace kdl {
 
 enum { MODE_PW = 0, MODE_CONV = 1, MODE_DW = 2 };
 
-template <int MODE, int FM, int FN, int WGM, int WGN>
+// DT: element type (common.h Elt): 0 bf16, 1 fp16 (MODE_PW / MODE_CONV only)
+template <int MODE, int FM, int FN, int WGM, int WGN, int DT = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs a) {
+  using E = Elt<DT>;
+  static_assert(MODE != MODE_DW || DT == 0, "the fused depthwise producer is bf16-only");
   constexpr int NW = WGM * WGN;
   constexpr int NT = 64 * NW;
   constexpr int BM = 16 * FM * WGM;
@@ -212,7 +215,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs 
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bc[j], af[i], acc[i][j]);
+      for (int j = 0; j < FN; ++j) acc[i][j] = E::mfma(bc[j], af[i], acc[i][j]);
     if constexpr (MODE == MODE_DW) {
       if (more) dw_compute(t + 1, cur ^ 1);
     }
@@ -236,7 +239,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs 
       if (a.relu_out == 1) {
         v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       }
-      u32x2 pk = {pack_bf16(v0, v1), pack_bf16(v2, v3)};
+      u32x2 pk = {E::pack(v0, v1), E::pack(v2, v3)};
       *(u32x2*)(smem + ml * CS + nl * 2) = pk;
     }
   }
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs 
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
     if (m < a.M && n < a.nstore) {
-      epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+      epi_store<DT>(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
     }
   }
 }
@@ -266,20 +269,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs 
   X(8, 8, 2, 1, 4)      \
   X(9, 4, 2, 1, 4)
 
-template <int MODE, int FM, int FN, int WGM, int WGN>
+template <int MODE, int FM, int FN, int WGM, int WGN, int DT>
 static hipError_t launch_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
   const int nM = (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
-  hipLaunchKernelGGL((conv_gemm_kernel<MODE, FM, FN, WGM, WGN>), dim3(nM * nN), dim3(64 * WGM * WGN), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<MODE, FM, FN, WGM, WGN, DT>), dim3(nM * nN), dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();
 }
 
-template <int MODE>
+template <int MODE, int DT = 0>
 static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   switch (cfg) {
 #define KDL_CASE(id, fm, fn, wgm, wgn) \
-  case id: return launch_cfg<MODE, fm, fn, wgm, wgn>(a, s);
+  case id: return launch_cfg<MODE, fm, fn, wgm, wgn, DT>(a, s);
     KDL_CONFIGS(KDL_CASE)
 #undef KDL_CASE
     default: return hipErrorInvalidValue;
@@ -287,7 +290,14 @@ static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 }
 
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
-  if (a.K % 32 != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (a.K % 32 != 0 || a.M <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+  if (a.dt == 1) {   // fp16: the pointwise / implicit-3x3 GEMMs only
+    if (cfg >= SEP_CFG_BASE) return hipErrorInvalidValue;
+    if (cfg >= PIPE_CFG_BASE) return gemm_pipe(mode, cfg - PIPE_CFG_BASE, a, s);
+    if (mode == MODE_PW) return launch_mode<MODE_PW, 1>(cfg, a, s);
+    if (mode == MODE_CONV) return launch_mode<MODE_CONV, 1>(cfg, a, s);
+    return hipErrorInvalidValue;
+  }
   if (cfg >= S2D_CFG_BASE) return mode == MODE_DW ? sepconv_2d(cfg - S2D_CFG_BASE, a, s) : hipErrorInvalidValue;
   if (cfg >= SEPP_CFG_BASE) return mode == MODE_DW ? sepconv_pipe(cfg - SEPP_CFG_BASE, a, s) : hipErrorInvalidValue;
   if (cfg >= SEP_CFG_BASE) return mode == MODE_DW ? sepconv_fused(cfg - SEP_CFG_BASE, a, s) : hipErrorInvalidValue;

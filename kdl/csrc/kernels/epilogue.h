@@ -25,10 +25,11 @@ __device__ __forceinline__ long out_offset(const ConvGemmArgs& a, int m) {
 // NOT on the MFMA accumulators: expanding erff/expf over every accumulator
 // element of every fragment grew the GEMM from ~700 to ~4000 instructions and
 // cost 15-30 % on GEMMs that never use them. ReLU (1) stays on the accumulators.
+template <int DT = 0>
 __device__ __noinline__ u32x4 act_transcendental(int mode, u32x4 v) {
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    float lo = bf_lo(v[d]), hi = bf_hi(v[d]);
+    float lo = Elt<DT>::lo(v[d]), hi = Elt<DT>::hi(v[d]);
     if (mode == 3) {
       lo = 0.5f * lo * (1.f + erff(lo * 0.70710678118654752f));
       hi = 0.5f * hi * (1.f + erff(hi * 0.70710678118654752f));
@@ -36,18 +37,21 @@ __device__ __noinline__ u32x4 act_transcendental(int mode, u32x4 v) {
       lo = lo / (1.f + __expf(-lo));
       hi = hi / (1.f + __expf(-hi));
     }
-    v[d] = pack_bf16(lo, hi);
+    v[d] = Elt<DT>::pack(lo, hi);
   }
   return v;
 }
 
-// v: 8 bf16 (bias + optional pre-residual ReLU already applied) for row m, cols n..n+7
+// v: 8 bf16 / fp16 (DT) values (bias + optional pre-residual ReLU already applied) for
+// row m, cols n..n+7
+template <int DT = 0>
 __device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u32x4 v) {
-  if (a.relu_out >= 3) v = act_transcendental(a.relu_out, v);
+  using E = Elt<DT>;
+  if (a.relu_out >= 3) v = act_transcendental<DT>(a.relu_out, v);
   if (a.res) {
     const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
 #pragma unroll
-    for (int d = 0; d < 4; ++d) v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
+    for (int d = 0; d < 4; ++d) v[d] = E::pack(E::lo(v[d]) + E::lo(rv[d]), E::hi(v[d]) + E::hi(rv[d]));
   }
   if (a.relu_out == 2) {
 #pragma unroll

@@ -8,7 +8,9 @@
 namespace kdl {
 
 // one block per image, one thread per 8-channel chunk (loops if F > 2048)
+template <int DT>
 __global__ __launch_bounds__(256) void gap_kernel(GapArgs a) {
+  using E = Elt<DT>;
   const int b = blockIdx.x;
   const uint16_t* xb = a.x + (long)b * a.HW * a.ldx;
   const float inv = 1.f / (float)a.HW;
@@ -18,8 +20,8 @@ __global__ __launch_bounds__(256) void gap_kernel(GapArgs a) {
       const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx + c8 * 8);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        s[2 * d] += bf_lo(v[d]);
-        s[2 * d + 1] += bf_hi(v[d]);
+        s[2 * d] += E::lo(v[d]);
+        s[2 * d + 1] += E::hi(v[d]);
       }
     }
     if (a.y) {
@@ -30,15 +32,16 @@ __global__ __launch_bounds__(256) void gap_kernel(GapArgs a) {
     if (a.yb) {
       u32x4 o;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) o[d] = pack_bf16(s[2 * d] * inv, s[2 * d + 1] * inv);
+      for (int d = 0; d < 4; ++d) o[d] = E::pack(s[2 * d] * inv, s[2 * d + 1] * inv);
       *(u32x4*)(a.yb + (long)b * a.F + c8 * 8) = o;
     }
   }
 }
 
 hipError_t gap(const GapArgs& a, hipStream_t s) {
-  if (a.F % 8 != 0 || a.ldx % 8 != 0 || a.B <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gap_kernel, dim3(a.B), dim3(256), 0, s, a);
+  if (a.F % 8 != 0 || a.ldx % 8 != 0 || a.B <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+  if (a.dt) hipLaunchKernelGGL(gap_kernel<1>, dim3(a.B), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(gap_kernel<0>, dim3(a.B), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -96,7 +99,9 @@ hipError_t fc(const FcArgs& a, hipStream_t s) {
 // waves split K four ways (each streams its B fragments and the A rows straight
 // from global/L2: every operand is used once per block) and the partial
 // accumulators are summed through LDS. 63 blocks for a 1000-class head.
+template <int DT>
 __global__ __launch_bounds__(256) void fc_mfma_kernel(FcMfmaArgs a) {
+  using E = Elt<DT>;
   __shared__ __attribute__((aligned(16))) float red[4][4][64][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nf = blockIdx.x, r0 = blockIdx.y * 64;
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(256) void fc_mfma_kernel(FcMfmaArgs a) {
     for (int i = 0; i < 4; ++i) {
       if (i < nm) {
         const s16x8 af = *(const s16x8*)(xb + (long)i * 16 * a.F + kt * 32);
-        acc[i] = mfma16(bf, af, acc[i]);
+        acc[i] = E::mfma(bf, af, acc[i]);
       }
     }
   }
@@ -143,9 +148,10 @@ __global__ __launch_bounds__(256) void fc_mfma_kernel(FcMfmaArgs a) {
 }
 
 hipError_t fc_mfma(const FcMfmaArgs& a, hipStream_t s) {
-  if (a.B <= 0 || a.F % 32 != 0 || a.NF * 16 < a.N) return hipErrorInvalidValue;
+  if (a.B <= 0 || a.F % 32 != 0 || a.NF * 16 < a.N || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
   const dim3 grid(a.NF, ((a.B + 15) / 16 + 3) / 4);
-  hipLaunchKernelGGL(fc_mfma_kernel, grid, dim3(256), 0, s, a);
+  if (a.dt) hipLaunchKernelGGL(fc_mfma_kernel<1>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(fc_mfma_kernel<0>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

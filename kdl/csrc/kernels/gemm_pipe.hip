@@ -33,8 +33,10 @@ __device__ __forceinline__ void wait_vm_barrier() {
 //   64 no B DMA, 128 rotate the k order per workgroup (a real variant: workgroups
 //   sharing the weights start at different k-steps instead of all requesting the same
 //   weight fragments at once)
-template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int ABL = 0>
+// DT: element type (common.h Elt): 0 bf16, 1 fp16
+template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int ABL = 0, int DT = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs a) {
+  using E = Elt<DT>;
   constexpr int NW = WGM * WGN;
   constexpr int BM = 16 * FM * WGM;
   constexpr int BN = 16 * FN * WGN;
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+          for (int j = 0; j < FN; ++j) acc[i][j] = E::mfma(bf[j], af[i], acc[i][j]);
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       if (a.relu_out == 1) {
         v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       }
-      *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
+      *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){E::pack(v0, v1), E::pack(v2, v3)};
     }
   }
   __syncthreads();
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       if constexpr (ABL & 4) {
         if (smem[r * CS + cc * 16] == 0x7f && smem[r * CS + cc * 16 + 1] == 0x7f) a.y[0] = 1;   // keep the tile live
       } else {
-        epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+        epi_store<DT>(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
       }
     }
   }
@@ -254,25 +256,32 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   X(43, 6, 3, 2, 4, 3, 1, 141) \
   X(44, 6, 3, 2, 4, 3, 1, 128)
 
-template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int ABL = 0>
+template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int ABL = 0, int DT = 0>
 static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
   const int nM = (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, ABL>), dim3(nM * nN), dim3(64 * WGM * WGN), 0,
-                     s, a);
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, ABL, DT>), dim3(nM * nN),
+                     dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();
 }
 
-template <int MODE>
+template <int MODE, int DT>
 static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   switch (cfg) {
 #define KDL_PCASE(id, fm, fn, wgm, wgn, st, ks) \
-  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks>(a, s);
+  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, 0, DT>(a, s);
     KDL_PIPE_CONFIGS(KDL_PCASE)
 #undef KDL_PCASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// timing ablations: pointwise mode, bf16 only
+static hipError_t launch_pipe_ablation(int cfg, const ConvGemmArgs& a, hipStream_t s) {
+  switch (cfg) {
 #define KDL_PACASE(id, fm, fn, wgm, wgn, st, ks, abl) \
-  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, abl>(a, s);
+  case id: return launch_pipe_cfg<0, fm, fn, wgm, wgn, st, ks, abl, 0>(a, s);
     KDL_PIPE_ABL(KDL_PACASE)
 #undef KDL_PACASE
     default: return hipErrorInvalidValue;
@@ -280,9 +289,10 @@ static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s
 }
 
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
-  if (a.K % 32 != 0 || a.M <= 0) return hipErrorInvalidValue;
-  if (mode == 0) return launch_pipe_mode<0>(cfg, a, s);
-  if (mode == 1 && cfg < 27) return launch_pipe_mode<1>(cfg, a, s);
+  if (a.K % 32 != 0 || a.M <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+  if (cfg >= 27) return mode == 0 && a.dt == 0 ? launch_pipe_ablation(cfg, a, s) : hipErrorInvalidValue;
+  if (mode == 0) return a.dt ? launch_pipe_mode<0, 1>(cfg, a, s) : launch_pipe_mode<0, 0>(cfg, a, s);
+  if (mode == 1) return a.dt ? launch_pipe_mode<1, 1>(cfg, a, s) : launch_pipe_mode<1, 0>(cfg, a, s);
   return hipErrorInvalidValue;
 }
 

@@ -32,6 +32,7 @@ struct ConvGemmArgs {
   int opad;              // 1: write into the interior of a 1-pixel zero-bordered output buffer, so the
                          //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
                          // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
+  int dt;                // element type of x / wp / res / y: 0 bf16, 1 fp16 (MODE_PW / MODE_CONV GEMMs)
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
@@ -84,6 +85,7 @@ struct StemArgs {
   float scale[3], shift[3];       // per-channel input normalisation applied on load (zero padding
                                   // stays exact: padded taps are 0 in the normalised space)
   int relu;                       // 0 none, 1 ReLU, 2 SiLU
+  int dt;                         // output element type: 0 bf16, 1 fp16
 };
 hipError_t stem_conv(const StemArgs& a, hipStream_t s);
 
@@ -94,6 +96,7 @@ struct PoolAddArgs {
   uint16_t* y;            // [B][OH][OW][C]
   int B, H, W, OH, OW, C; // C multiple of 8
   int pad_top, pad_left;
+  int dt;                 // element type: 0 bf16, 1 fp16
 };
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s);
 
@@ -103,6 +106,7 @@ struct GapArgs {
   float* y;               // [B][F] fp32 (may be null)
   uint16_t* yb;           // [B][F] bf16 copy for the MFMA classifier (may be null)
   int B, HW, ldx, F;      // F multiple of 8
+  int dt;                 // element type of x and yb: 0 bf16, 1 fp16
 };
 hipError_t gap(const GapArgs& a, hipStream_t s);
 
@@ -124,6 +128,7 @@ struct FcMfmaArgs {
   const float* bias;
   float* out;
   int B, F, N, NF, relu;
+  int dt;                 // element type of xb and wp: 0 bf16, 1 fp16
 };
 hipError_t fc_mfma(const FcMfmaArgs& a, hipStream_t s);
 

@@ -9,7 +9,9 @@ namespace kdl {
 // One thread = one output pixel x 8 channels. TF 'same' pads with -inf, i.e.
 // out-of-range taps are skipped (the odd pad goes bottom/right: pad_top/left
 // are the *leading* pads computed on the host).
+template <int DT>
 __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
+  using E = Elt<DT>;
   const int CC = a.C >> 3;
   const long total = (long)a.B * a.OH * a.OW * CC;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -34,8 +36,8 @@ __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
       const u32x4 v = *(const u32x4*)(a.x + (((long)b * a.H + ih) * a.W + iw) * a.C + cc * 8);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        mx[2 * d] = fmaxf(mx[2 * d], bf_lo(v[d]));
-        mx[2 * d + 1] = fmaxf(mx[2 * d + 1], bf_hi(v[d]));
+        mx[2 * d] = fmaxf(mx[2 * d], E::lo(v[d]));
+        mx[2 * d + 1] = fmaxf(mx[2 * d + 1], E::hi(v[d]));
       }
     }
   }
@@ -43,20 +45,21 @@ __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
     const u32x4 r = *(const u32x4*)(a.res + p * a.C + cc * 8);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      mx[2 * d] += bf_lo(r[d]);
-      mx[2 * d + 1] += bf_hi(r[d]);
+      mx[2 * d] += E::lo(r[d]);
+      mx[2 * d + 1] += E::hi(r[d]);
     }
   }
   u32x4 o;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) o[d] = pack_bf16(mx[2 * d], mx[2 * d + 1]);
+  for (int d = 0; d < 4; ++d) o[d] = E::pack(mx[2 * d], mx[2 * d + 1]);
   *(u32x4*)(a.y + p * a.C + cc * 8) = o;
 }
 
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
-  if (a.C % 8 != 0) return hipErrorInvalidValue;
+  if (a.C % 8 != 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
   const long total = (long)a.B * a.OH * a.OW * (a.C / 8);
-  hipLaunchKernelGGL(pool_add_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  if (a.dt) hipLaunchKernelGGL(pool_add_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(pool_add_kernel<0>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

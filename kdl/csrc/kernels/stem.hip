@@ -18,8 +18,9 @@ namespace kdl {
 
 // GENERIC=false: 'valid' conv with the normalisation folded into the weights (the
 // Xception stem): no bounds checks, no per-element scale/shift.
-template <int IN_KIND, int NF, int KW, bool GENERIC>
+template <int IN_KIND, int NF, int KW, bool GENERIC, int DT = 0>
 __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
+  using E = Elt<DT>;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int M = a.B * a.OH * a.OW;
   const int OHW = a.OH * a.OW;
@@ -79,10 +80,10 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
             v = raw;
           }
         }
-        af[j] = (short)f2bf(v);
+        af[j] = (short)E::from_f32(v);
       }
 #pragma unroll
-      for (int j = 0; j < NF; ++j) acc[f][j] = mfma16(bw[j], af, acc[f][j]);
+      for (int j = 0; j < NF; ++j) acc[f][j] = E::mfma(bw[j], af, acc[f][j]);
     }
   }
   // lane holds Y[m_tile + (lane&15)][16j + 4*(lane>>4) + r]. The block's 128 output
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
         v0 = v0 / (1.f + __expf(-v0)); v1 = v1 / (1.f + __expf(-v1));
         v2 = v2 / (1.f + __expf(-v2)); v3 = v3 / (1.f + __expf(-v3));
       }
-      *(u32x2*)(ys + ml * NF * 16 + n) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
+      *(u32x2*)(ys + ml * NF * 16 + n) = (u32x2){E::pack(v0, v1), E::pack(v2, v3)};
     }
   }
   __syncthreads();
@@ -121,6 +122,12 @@ template <int IN_KIND, int KW>
 static hipError_t launch_stem(const StemArgs& a, dim3 grid, hipStream_t s) {
   const bool generic = a.pad != 0 || a.scale[0] != 1.f || a.scale[1] != 1.f || a.scale[2] != 1.f ||
                        a.shift[0] != 0.f || a.shift[1] != 0.f || a.shift[2] != 0.f;
+  if (a.dt == 1) {   // fp16 (ResNet-50 fp16 config): the 64-channel normalise-on-load stem only
+    if (a.cout != 64 || !generic) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((stem_kernel<IN_KIND, 4, KW, true, 1>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  if (a.dt != 0) return hipErrorInvalidValue;
   if (a.cout == 32 && !generic) hipLaunchKernelGGL((stem_kernel<IN_KIND, 2, KW, false>), grid, dim3(256), 0, s, a);
   else if (a.cout == 32) hipLaunchKernelGGL((stem_kernel<IN_KIND, 2, KW, true>), grid, dim3(256), 0, s, a);
   else if (a.cout == 64 && !generic) hipLaunchKernelGGL((stem_kernel<IN_KIND, 4, KW, false>), grid, dim3(256), 0, s, a);

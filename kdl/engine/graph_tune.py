@@ -121,9 +121,10 @@ def main(argv=None) -> int:
         eng = LaneGroup(info, params, a.batch, dev, a.lanes)
     else:
         eng = info.engine(params, a.batch, dev)
-    start = Path(a.start) if a.start else tuning_path(a.model, a.batch, a.lanes)
+    tname = info.tuning or a.model
+    start = Path(a.start) if a.start else tuning_path(tname, a.batch, a.lanes)
     if not start.exists():
-        start = tuning_path(a.model, a.batch)
+        start = tuning_path(tname, a.batch)
     eng.load_tuning(start)
     # random input (DVFS / MFMA clock behaviour differs on zeros)
     g = torch.Generator().manual_seed(0)

@@ -18,6 +18,8 @@ class ModelInfo:
     init_params: Callable
     engine: Callable          # (params, max_batch, device, **kw) -> EngineBase
     oracle: Callable          # (params, uint8 NHWC) -> fp32 logits
+    dtype: str = "bf16"       # compute dtype of the engine (bench.py's "dtype" field)
+    tuning: str = ""          # tuning-table family name when it differs from ``name``
 
 
 def _xception():
@@ -31,14 +33,17 @@ def _xception():
                      lambda p, x: X.xception_forward(p, x.float() / 127.5 - 1.0))
 
 
-def _resnet50():
+def _resnet50(dtype: str = "fp16"):
+    """BASELINE.json config 3 is "ResNet-50 224x224 fp16": fp16 by default,
+    ``resnet50_bf16`` for the bf16 variant (same kernels, v_mfma_*_bf16)."""
     from ..models import resnet as R
     from .resnet import ResNetEngine
-    return ModelInfo("resnet50", R.INPUT_SIZE, 1000, R.TOTAL_PARAMS,
-                     "ResNet-50 v1.5 224x224 (torchvision layout, 25,557,032 params)",
+    return ModelInfo("resnet50" if dtype == "fp16" else "resnet50_bf16", R.INPUT_SIZE, 1000, R.TOTAL_PARAMS,
+                     f"ResNet-50 v1.5 224x224 (torchvision layout, 25,557,032 params), {dtype}",
                      lambda seed=0: R.init_params(seed=seed),
-                     lambda p, max_batch, device, **kw: ResNetEngine(p, max_batch=max_batch, device=device, **kw),
-                     R.resnet_forward)
+                     lambda p, max_batch, device, **kw: ResNetEngine(p, max_batch=max_batch, device=device,
+                                                                     dtype=dtype, **kw),
+                     R.resnet_forward, dtype=dtype, tuning="resnet50")
 
 
 def _vit_b16():
@@ -70,11 +75,11 @@ def _vit_b16_fp8():
                      lambda seed=0: V.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: ViTEngine(p, max_batch=max_batch, device=device, fp8=True,
                                                                   **kw),
-                     V.vit_forward)
+                     V.vit_forward, dtype="fp8-e4m3 linears / bf16 rest")
 
 
-_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "vit_b16": _vit_b16, "vit_b16_fp8": _vit_b16_fp8,
-              "efficientnet_b7": _efficientnet_b7}
+_FACTORIES = {"xception": _xception, "resnet50": _resnet50, "resnet50_bf16": lambda: _resnet50("bf16"),
+              "vit_b16": _vit_b16, "vit_b16_fp8": _vit_b16_fp8, "efficientnet_b7": _efficientnet_b7}
 
 
 def models() -> list[str]:

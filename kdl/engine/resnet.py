@@ -44,10 +44,16 @@ class ResNetEngine(EngineBase):
     model_name = "resnet50"
 
     def __init__(self, params: dict, max_batch: int = 32, device: str | torch.device = "cuda",
-                 in_kind: str = "u8", buckets=None, tune_file: str | Path | None = None):
+                 in_kind: str = "u8", buckets=None, tune_file: str | Path | None = None,
+                 dtype: str = "fp16"):
+        """``dtype``: "fp16" (BASELINE.json's "ResNet-50 224x224 fp16" config: IEEE half
+        activations and weights on v_mfma_f32_16x16x32_f16, fp32 accumulation) or "bf16"."""
         super().__init__(device, max_batch, buckets)
         assert in_kind in ("u8", "f32")
+        assert dtype in ("fp16", "bf16"), dtype
         self.in_kind = in_kind
+        self.dtype = torch.float16 if dtype == "fp16" else torch.bfloat16
+        self.dt = int(dtype == "fp16")
         self.size = R.INPUT_SIZE
         self.classes = params["fc.bias"].numel()
         self.shapes: dict[str, tuple[int, int, int, int]] = {}   # buffer -> (H, W, C, border)
@@ -62,7 +68,7 @@ class ResNetEngine(EngineBase):
         S = self.size
         # stem: 7x7/2 pad 3, K = 147 (k = tap*3 + c) padded to 160
         w, t = _fold(p, "conv1.weight", "bn1")
-        self.stem_wp = pack_fragments(w, 4, 5).to(dev).contiguous()
+        self.stem_wp = pack_fragments(w, 4, 5, self.dtype).to(dev).contiguous()
         self.stem_bias = t.float().to(dev)
         oh = (S + 6 - 7) // 2 + 1                                   # 112
         self.steps.append(Step("stem", "conv1", src="input", dst="stem", geom=(S, S, oh, oh)))
@@ -80,18 +86,18 @@ class ResNetEngine(EngineBase):
             self.shapes[tmid] = (oh, oh, wdt, 0)
             w1, b1 = _fold(p, f"{blk.prefix}.conv1.weight", f"{blk.prefix}.bn1")
             l1 = ConvGemmLayer(f"{blk.prefix}.conv1", MODE_PW, w1, b1, cin_pad=blk.cin, n=wdt,
-                               relu_out=1, device=dev)
+                               relu_out=1, device=dev, dtype=self.dtype)
             self.steps.append(Step("conv", l1.name, l1, cur, tpad, geom=(H, H, H, H), extra=dict(opad=1)))
             w2, b2 = _fold(p, f"{blk.prefix}.conv2.weight", f"{blk.prefix}.bn2")
             l2 = ConvGemmLayer(f"{blk.prefix}.conv2", MODE_CONV, w2, b2, cin_pad=wdt, n=wdt,
-                               stride=blk.stride, relu_out=1, device=dev)
+                               stride=blk.stride, relu_out=1, device=dev, dtype=self.dtype)
             self.steps.append(Step("conv", l2.name, l2, tpad, tmid, geom=(H + 2, H + 2, oh, oh)))
             if blk.downsample:
                 sc = f"sc{oh}_{cout}"
                 self.shapes[sc] = (oh, oh, cout, 0)
                 wd, bd = _fold(p, f"{blk.prefix}.downsample.0.weight", f"{blk.prefix}.downsample.1")
                 ld = ConvGemmLayer(f"{blk.prefix}.downsample", MODE_PW, wd, bd, cin_pad=blk.cin, n=cout,
-                                   stride=blk.stride, device=dev)
+                                   stride=blk.stride, device=dev, dtype=self.dtype)
                 self.steps.append(Step("conv", ld.name, ld, cur, sc, geom=(H, H, oh, oh)))
                 res = sc
             else:
@@ -101,11 +107,11 @@ class ResNetEngine(EngineBase):
             self.shapes[out] = (oh, oh, cout, 0)
             w3, b3 = _fold(p, f"{blk.prefix}.conv3.weight", f"{blk.prefix}.bn3")
             l3 = ConvGemmLayer(f"{blk.prefix}.conv3", MODE_PW, w3, b3, cin_pad=wdt, n=cout, relu_out=2,
-                               device=dev)
+                               device=dev, dtype=self.dtype)
             self.steps.append(Step("conv", l3.name, l3, tmid, out, res=res, geom=(oh, oh, oh, oh)))
             cur, H = out, oh
         nf = (self.classes + 15) // 16
-        self.fc_wp = pack_fragments(p["fc.weight"].float(), nf, 2048 // 32).to(dev).contiguous()
+        self.fc_wp = pack_fragments(p["fc.weight"].float(), nf, 2048 // 32, self.dtype).to(dev).contiguous()
         self.fc_nf = nf
         self.fc_b = p["fc.bias"].float().to(dev)
         self.steps.append(Step("gap", "avgpool", src=cur, dst="feat", geom=(H, H, 1, 1), extra=dict(F=2048)))
@@ -118,8 +124,8 @@ class ResNetEngine(EngineBase):
         self.bufs: dict[str, torch.Tensor] = {}
         for name, (h, w, c, border) in self.shapes.items():
             n = B * (h + 2 * border) * (w + 2 * border) * c
-            self.bufs[name] = torch.zeros(n, dtype=torch.bfloat16, device=dev)   # borders stay 0
-        self.feat = torch.zeros(((B + 15) // 16 * 16, 2048), dtype=torch.bfloat16, device=dev)
+            self.bufs[name] = torch.zeros(n, dtype=self.dtype, device=dev)   # borders stay 0
+        self.feat = torch.zeros(((B + 15) // 16 * 16, 2048), dtype=self.dtype, device=dev)
         self.logits = torch.zeros((B, self.classes), dtype=torch.float32, device=dev)
 
     # ------------------------------------------------------------------ emission
@@ -155,20 +161,21 @@ class ResNetEngine(EngineBase):
                                           in_kind=0 if self.in_kind == "u8" else 1,
                                           KH=7, KW=7, stride=2, pad=3, cout=64, relu=1,
                                           scale0=sc[0], scale1=sc[1], scale2=sc[2],
-                                          shift0=sh[0], shift1=sh[1], shift2=sh[2]))
+                                          shift0=sh[0], shift1=sh[1], shift2=sh[2], dt=self.dt))
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=None, y=self._ptr(step.dst),
                                               B=b, H=H, W=W, OH=OH, OW=OW, C=step.extra["C"],
-                                              pad_top=1, pad_left=1))
+                                              pad_top=1, pad_left=1, dt=self.dt))
         elif step.kind == "conv":
             self._emit_conv(prog, step, b)
         elif step.kind == "gap":
             prog.add_gap(step.name, dict(x=self._ptr(step.src), y=None, yb=self._ptr("feat"), B=b, HW=H * W,
-                                         ldx=self._ld(step.src), F=step.extra["F"]))
+                                         ldx=self._ld(step.src), F=step.extra["F"], dt=self.dt))
         elif step.kind == "fc":
             prog.add_fc_mfma(step.name, dict(xb=self._ptr("feat"), wp=_lib.ptr(self.fc_wp),
                                              bias=_lib.ptr(self.fc_b), out=self._ptr("logits"), B=b,
-                                             F=step.extra["F"], N=self.classes, NF=self.fc_nf, relu=0))
+                                             F=step.extra["F"], N=self.classes, NF=self.fc_nf, relu=0,
+                                             dt=self.dt))
         else:  # pragma: no cover
             raise ValueError(step.kind)
 

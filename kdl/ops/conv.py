@@ -159,7 +159,12 @@ class ConvGemmLayer:
     def __init__(self, name: str, mode: int, w_nk: torch.Tensor, bias: torch.Tensor, *,
                  cin_pad: int, n: int, stride: int = 1, dww: torch.Tensor | None = None,
                  relu_in: bool = False, relu_out: bool | int = False, device="cuda",
-                 candidates: list[int] | None = None):
+                 candidates: list[int] | None = None, dtype: torch.dtype = torch.bfloat16):
+        """``dtype``: element type of the activations and packed weights, bf16 (default)
+        or fp16 (MODE_PW / MODE_CONV only; ``dt`` = 1 in the launch args)."""
+        assert dtype in (torch.bfloat16, torch.float16), dtype
+        assert dtype == torch.bfloat16 or mode != MODE_DW, "fused separable convs are bf16-only"
+        self.dtype, self.dt = dtype, int(dtype == torch.float16)
         self.name, self.mode, self.n = name, mode, n
         self.cin_pad, self.stride = cin_pad, stride
         # relu_out: 0/False none, 1/True ReLU before the residual add, 2 ReLU after it
@@ -172,7 +177,7 @@ class ConvGemmLayer:
         self.cfg = default_config(mode, n, 0) if candidates is None else self.candidates[0]
         if self.cfg not in self.candidates:
             self.cfg = self.candidates[0]
-        self.wp = pack_fragments(w_nk, self.nf_max, self.K // 32).to(device).contiguous()
+        self.wp = pack_fragments(w_nk, self.nf_max, self.K // 32, dtype).to(device).contiguous()
         self.bias = pad_vec(bias, self.nf_max * 16).to(device)
         self.dww = None
         self.dwk = None
@@ -181,7 +186,7 @@ class ConvGemmLayer:
             self.dww = dww.float().contiguous().to(device)
             self.dwk = pack_dw_entries(dww).to(device)
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
-        self.w_ref = w_nk.to(torch.bfloat16).float()
+        self.w_ref = w_nk.to(dtype).float()
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
         # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
         self.split = False
@@ -238,7 +243,7 @@ class ConvGemmLayer:
                     ldr=ldr if ldr is not None else self.ldy,
                     K=self.K, cin=self.cin_pad, NF=self.nf(cfg), nstore=self.ldy,
                     stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out),
-                    opad=int(opad))
+                    opad=int(opad), dt=self.dt)
 
     def launch(self, x: torch.Tensor, y: torch.Tensor, g: Geometry, res: torch.Tensor | None = None,
                cfg: int | None = None, split: bool = False, tmp: torch.Tensor | None = None,
@@ -253,7 +258,7 @@ class ConvGemmLayer:
                   opad=opad)
 
     def check(self, x, y, g: Geometry, res=None, opad: int = 0) -> None:
-        assert x.dtype == torch.bfloat16 and y.dtype == torch.bfloat16
+        assert x.dtype == self.dtype and y.dtype == self.dtype, (x.dtype, y.dtype, self.dtype)
         assert x.is_contiguous() and y.is_contiguous()
         assert x.numel() >= g.B * g.H * g.W * self.cin_pad, (self.name, x.shape)
         assert y.numel() >= g.B * (g.OH + 2 * opad) * (g.OW + 2 * opad) * self.ldy, (self.name, y.shape)
@@ -264,7 +269,7 @@ class ConvGemmLayer:
         else:
             assert g.OH == (g.H - 1) // self.stride + 1 and g.OW == (g.W - 1) // self.stride + 1
         if res is not None:
-            assert res.dtype == torch.bfloat16 and res.numel() >= g.M * self.ldy
+            assert res.dtype == self.dtype and res.numel() >= g.M * self.ldy
 
 
 def pack_dw_entries(dww: torch.Tensor) -> torch.Tensor:

@@ -24,15 +24,15 @@ def bn_scale_shift(p: dict, bn: str, eps: float = KERAS_BN_EPS):
     return s, b - m * s
 
 
-def pack_fragments(w_nk: torch.Tensor, nf: int, kt: int) -> torch.Tensor:
-    """W[N][K] (any float dtype) -> bf16 [nf][kt][64][8] zero padded."""
+def pack_fragments(w_nk: torch.Tensor, nf: int, kt: int, dtype: torch.dtype = torch.bfloat16) -> torch.Tensor:
+    """W[N][K] (any float dtype) -> ``dtype`` (bf16 or fp16) [nf][kt][64][8] zero padded."""
     n, k = w_nk.shape
     assert n <= nf * 16 and k <= kt * 32, (w_nk.shape, nf, kt)
     full = torch.zeros(nf * 16, kt * 32, dtype=torch.float32)
     full[:n, :k] = w_nk.float()
     # [nf, 16(r), kt, 4(q), 8(j)] -> [nf, kt, q, r, j] ; lane = q*16 + r
     t = full.view(nf, 16, kt, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
-    return t.view(nf, kt, 64, 8).to(torch.bfloat16)
+    return t.view(nf, kt, 64, 8).to(dtype)
 
 
 def unpack_fragments(packed: torch.Tensor, n: int, k: int) -> torch.Tensor:

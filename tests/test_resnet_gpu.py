@@ -19,72 +19,75 @@ def _rel(a, b):
     return ((a.float() - b).abs().max() / b.abs().max()).item()
 
 
-def test_stem_7x7_normalise_on_load():
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_stem_7x7_normalise_on_load(dt):
     gen = torch.Generator().manual_seed(0)
     B, S = 2, 64
     x = torch.randint(0, 256, (B, S, S, 3), generator=gen, dtype=torch.uint8)
     w = torch.randn(64, 3, 7, 7, generator=gen) * 0.1
     bias = torch.randn(64, generator=gen) * 0.1
     wnk = w.permute(0, 2, 3, 1).reshape(64, 147)
-    wp = pack_fragments(wnk, 4, 5).to(DEV)
+    wp = pack_fragments(wnk, 4, 5, dt).to(DEV)
     OH = (S + 6 - 7) // 2 + 1
-    y = torch.zeros(B * OH * OH * 64, dtype=torch.bfloat16, device=DEV)
+    y = torch.zeros(B * OH * OH * 64, dtype=dt, device=DEV)
     sc = [1 / (255 * s) for s in R.STD]
     sh = [-m / s for m, s in zip(R.MEAN, R.STD)]
     xd, bd = x.to(DEV), bias.to(DEV)
     _lib.lib().stem_conv(dict(x=xd.data_ptr(), wp=wp.data_ptr(), bias=bd.data_ptr(), y=y.data_ptr(),
                               B=B, H=S, W=S, OH=OH, OW=OH, ldy=64, in_kind=0, KH=7, KW=7, stride=2, pad=3,
                               cout=64, relu=1, scale0=sc[0], scale1=sc[1], scale2=sc[2], shift0=sh[0],
-                              shift1=sh[1], shift2=sh[2]), _lib.stream_ptr())
+                              shift1=sh[1], shift2=sh[2], dt=int(dt == torch.float16)), _lib.stream_ptr())
     torch.cuda.synchronize()
     xn = R.preprocess(x)
     ref = torch.relu(F.conv2d(xn, w, bias, stride=2, padding=3)).permute(0, 2, 3, 1)
     assert _rel(y.cpu().view(B, OH, OH, 64), ref) < 2e-2
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("stride", [1, 2])
-def test_padded_output_then_strided_3x3(stride):
+def test_padded_output_then_strided_3x3(stride, dt):
     """1x1 (opad=1) -> zero-bordered buffer -> 3x3/stride 'valid' == 3x3 'same' (pad 1)."""
     gen = torch.Generator().manual_seed(stride)
     B, H, C, N = 2, 14, 64, 64
-    x = torch.randn(B, H, H, C, generator=gen).to(torch.bfloat16)
+    x = torch.randn(B, H, H, C, generator=gen).to(dt)
     w1 = torch.randn(C, C, generator=gen, dtype=torch.float64) / C ** 0.5
     b1 = torch.randn(C, generator=gen) * 0.1
-    l1 = ConvGemmLayer("c1", MODE_PW, w1, b1, cin_pad=C, n=C, relu_out=1, device=DEV)
+    l1 = ConvGemmLayer("c1", MODE_PW, w1, b1, cin_pad=C, n=C, relu_out=1, device=DEV, dtype=dt)
     w2 = torch.randn(N, 3, 3, C, generator=gen, dtype=torch.float64) / (9 * C) ** 0.5
     b2 = torch.randn(N, generator=gen) * 0.1
     l2 = ConvGemmLayer("c2", MODE_CONV, w2.reshape(N, 9 * C), b2, cin_pad=C, n=N, stride=stride,
-                       relu_out=1, device=DEV)
+                       relu_out=1, device=DEV, dtype=dt)
     xd = x.to(DEV).contiguous()
-    tpad = torch.zeros(B * (H + 2) * (H + 2) * C, dtype=torch.bfloat16, device=DEV)
+    tpad = torch.zeros(B * (H + 2) * (H + 2) * C, dtype=dt, device=DEV)
     OH = (H + 2 - 3) // stride + 1
-    y = torch.zeros(B * OH * OH * N, dtype=torch.bfloat16, device=DEV)
+    y = torch.zeros(B * OH * OH * N, dtype=dt, device=DEV)
     for cfg in [c for _, c in l1.variants(H)][:4]:
         l1.launch(xd, tpad, Geometry(B, H, H, H, H), cfg=cfg, opad=1)
         for cfg2 in [c for _, c in l2.variants(H)][:4]:
             l2.launch(tpad, y, Geometry(B, H + 2, H + 2, OH, OH), cfg=cfg2)
             torch.cuda.synchronize()
             t = torch.relu(x.float().reshape(-1, C) @ w1.float().t() + b1).reshape(B, H, H, C)
-            t = t.to(torch.bfloat16).float().permute(0, 3, 1, 2)
+            t = t.to(dt).float().permute(0, 3, 1, 2)
             ref = torch.relu(F.conv2d(t, w2.float().permute(0, 3, 1, 2), b2, stride=stride, padding=1))
             assert _rel(y.cpu().view(B, OH, OH, N), ref.permute(0, 2, 3, 1)) < 2e-2, (cfg, cfg2)
             border = tpad.cpu().view(B, H + 2, H + 2, C)
             assert border[:, 0].abs().max() == 0 and border[:, :, -1].abs().max() == 0
 
 
-def test_relu_after_residual():
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_relu_after_residual(dt):
     gen = torch.Generator().manual_seed(3)
     B, H, C, N = 2, 7, 128, 256
-    x = torch.randn(B * H * H, C, generator=gen).to(torch.bfloat16)
-    r = torch.randn(B * H * H, N, generator=gen).to(torch.bfloat16)
+    x = torch.randn(B * H * H, C, generator=gen).to(dt)
+    r = torch.randn(B * H * H, N, generator=gen).to(dt)
     w = torch.randn(N, C, generator=gen, dtype=torch.float64) / C ** 0.5
     b = torch.randn(N, generator=gen) * 0.1
-    lay = ConvGemmLayer("c3", MODE_PW, w, b, cin_pad=C, n=N, relu_out=2, device=DEV)
-    y = torch.zeros(B * H * H * N, dtype=torch.bfloat16, device=DEV)
+    lay = ConvGemmLayer("c3", MODE_PW, w, b, cin_pad=C, n=N, relu_out=2, device=DEV, dtype=dt)
+    y = torch.zeros(B * H * H * N, dtype=dt, device=DEV)
     lay.launch(x.to(DEV).contiguous(), y, Geometry(B, H, H, H, H), res=r.to(DEV).contiguous())
     torch.cuda.synchronize()
     ref = torch.relu(x.float() @ w.float().t() + b + r.float())
-    assert _rel(y.cpu().view(-1, N), ref) < 2e-2
+    assert _rel(y.cpu().view(-1, N), ref) < (2e-2 if dt == torch.bfloat16 else 4e-3)
     assert (y.float() >= 0).all()
 
 
@@ -132,9 +135,10 @@ def _close(out, ref):
     assert _rel(out, ref) < 0.2
 
 
-def test_resnet_engine_matches_oracle(rparams):
+@pytest.mark.parametrize("dtype", ["fp16", "bf16"])
+def test_resnet_engine_matches_oracle(rparams, dtype):
     from kdl.engine.resnet import ResNetEngine
-    eng = ResNetEngine(rparams, max_batch=4, device=DEV, buckets=[2, 4])
+    eng = ResNetEngine(rparams, max_batch=4, device=DEV, buckets=[2, 4], dtype=dtype)
     gen = torch.Generator().manual_seed(7)
     x = torch.randint(0, 256, (3, 224, 224, 3), generator=gen, dtype=torch.uint8)
     ref = R.resnet_forward(rparams, x)
@@ -146,3 +150,35 @@ def test_resnet_engine_matches_oracle(rparams):
     eng.autotune(4, iters=2)
     out = eng.forward(x.to(DEV)).cpu()
     _close(out, ref)
+
+
+def test_fp16_gap_fc_and_pool():
+    """fp16 features + fp16 MFMA classifier, fp16 max-pool (the fp16 ResNet path)."""
+    gen = torch.Generator().manual_seed(5)
+    B, HW, Fd, N = 5, 49, 2048, 1000
+    x = torch.randn(B, HW, Fd, generator=gen).to(torch.float16).to(DEV)
+    w = (torch.randn(Fd, N, generator=gen) / Fd ** 0.5)
+    b = torch.randn(N, generator=gen).to(DEV)
+    C = _lib.lib()
+    s = _lib.stream_ptr()
+    fb = torch.zeros((B + 15) // 16 * 16, Fd, dtype=torch.float16, device=DEV)
+    C.gap(dict(x=x.data_ptr(), y=None, yb=fb.data_ptr(), B=B, HW=HW, ldx=Fd, F=Fd, dt=1), s)
+    nf = (N + 15) // 16
+    wp = pack_fragments(w.t(), nf, Fd // 32, torch.float16).to(DEV)
+    out = torch.zeros(B, N, device=DEV)
+    C.fc_mfma(dict(xb=fb.data_ptr(), wp=wp.data_ptr(), bias=b.data_ptr(), out=out.data_ptr(), B=B, F=Fd,
+                   N=N, NF=nf, relu=0, dt=1), s)
+    torch.cuda.synchronize()
+    assert _rel(fb[:B], x.float().mean(dim=1)) < 2e-3
+    ref = fb[:B].float() @ w.to(torch.float16).float().to(DEV) + b
+    assert _rel(out, ref) < 1e-3
+    # 3x3/2 max-pool, pad 1 (ResNet stem pool)
+    H, Cc = 15, 64
+    xp = torch.randn(2, H, H, Cc, generator=gen).to(torch.float16).to(DEV)
+    OH = (H + 2 - 3) // 2 + 1
+    yp = torch.zeros(2 * OH * OH * Cc, dtype=torch.float16, device=DEV)
+    C.pool_add(dict(x=xp.data_ptr(), res=None, y=yp.data_ptr(), B=2, H=H, W=H, OH=OH, OW=OH, C=Cc,
+                    pad_top=1, pad_left=1, dt=1), s)
+    torch.cuda.synchronize()
+    refp = F.max_pool2d(xp.float().permute(0, 3, 1, 2), 3, 2, padding=1).permute(0, 2, 3, 1)
+    assert torch.equal(yp.view(2, OH, OH, Cc).float(), refp)

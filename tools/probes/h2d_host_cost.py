@@ -82,3 +82,42 @@ for label, wait in (("idle copy stream", False), ("copy stream waits on busy wor
         torch.cuda.synchronize()
     ts.sort()
     print(f"{label:34s} host us: median {ts[5] * 1e6:8.1f}  max {ts[-1] * 1e6:8.1f}", flush=True)
+
+# Same, but the event follows a hipGraph replay (what bench.py's slots wait on)
+g_in = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+gs = torch.cuda.Stream()
+graph = torch.cuda.CUDAGraph()
+with torch.cuda.stream(gs):
+    y_ = g_in @ g_in
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph, stream=gs):
+        for _ in range(20):
+            y_ = (y_ @ g_in).clamp_(-1, 1)
+torch.cuda.synchronize()
+big = torch.zeros(64 * 1024 // 4, dtype=torch.float32).pin_memory()
+bigd = torch.zeros(64 * 1024 // 4, dtype=torch.float32, device="cuda")
+cases = {
+    "H2D 8.6 MB": lambda: hip.hipMemcpyAsync(d.data_ptr(), h.data_ptr(), h.numel(), 1, ctypes.c_void_p(cs.cuda_stream)),
+    "D2H 1.3 KB": lambda: hip.hipMemcpyAsync(lh.data_ptr(), lo.data_ptr(), lo.numel() * 4, 2, ctypes.c_void_p(cs.cuda_stream)),
+    "D2H 10 KB": lambda: hip.hipMemcpyAsync(big.data_ptr(), bigd.data_ptr(), 10240, 2, ctypes.c_void_p(cs.cuda_stream)),
+    "D2H 64 KB": lambda: hip.hipMemcpyAsync(big.data_ptr(), bigd.data_ptr(), 65536, 2, ctypes.c_void_p(cs.cuda_stream)),
+}
+for label, fn in cases.items():
+    for mode in ("idle", "wait-on-graph-event", "same-stream-after-graph"):
+        ts = []
+        for _ in range(8):
+            graph.replay() if mode != "idle" else None
+            if mode == "wait-on-graph-event":
+                with torch.cuda.stream(gs):
+                    graph.replay()
+                    ev.record(gs)
+                cs.wait_event(ev)
+            elif mode == "same-stream-after-graph":
+                with torch.cuda.stream(cs):
+                    graph.replay()
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+            torch.cuda.synchronize()
+        ts.sort()
+        print(f"{label:12s} {mode:26s} host us: median {ts[4] * 1e6:8.1f}  max {ts[-1] * 1e6:8.1f}", flush=True)
