@@ -46,6 +46,7 @@ class EngineBase:
         self.inputs: list[torch.Tensor] = []   # input slots (self.inp is slot 0)
         self.outputs: list[torch.Tensor] = []  # per-slot logits (self.logits is slot 0)
         self._slot = 0
+        self._remap: dict[str, str] = {}      # buffer-name overrides while emitting (stages.py)
 
     # ---------------------------------------------------------------- input slots
     def input_ptr(self) -> int:
@@ -97,6 +98,25 @@ class EngineBase:
                 self._emit(prog, step, b)
         finally:
             self._slot = 0
+        if capture:
+            with torch.cuda.device(self.device):
+                prog.capture(int(self.stream.cuda_stream))
+        self.programs[key] = prog
+        return prog
+
+    def program_range(self, b: int, lo: int, hi: int, capture: bool = True, slot: int = 0,
+                      remap: dict | None = None):
+        """Program of steps[lo:hi] only, with buffer names remapped (``stages.py``)."""
+        key = (b, capture, slot, lo, hi, tuple(sorted((remap or {}).items())))
+        if key in self.programs:
+            return self.programs[key]
+        prog = _lib.lib().Program()
+        self._slot, self._remap = slot, dict(remap or {})
+        try:
+            for step in self.steps[lo:hi]:
+                self._emit(prog, step, b)
+        finally:
+            self._slot, self._remap = 0, {}
         if capture:
             with torch.cuda.device(self.device):
                 prog.capture(int(self.stream.cuda_stream))

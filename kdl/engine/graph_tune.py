@@ -41,7 +41,19 @@ def _variants_of(eng, step):
 
 
 def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
-    """ms per forward replay (all lanes), after (re)capturing the graphs."""
+    """ms per forward replay (all lanes), after (re)capturing the graphs. Stage-pipelined
+    engines (``stages.StagePipe``) are timed free-running over two input slots, so
+    consecutive batches overlap as they do in bench.py."""
+    if getattr(eng, "pipelined", False):
+        done = [torch.cuda.Event(), torch.cuda.Event()]
+        for r in range(warm + 2):
+            eng.launch_async(b, [], [done[r % 2]], slot=r % 2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in range(reps):
+            eng.launch_async(b, [], [done[r % 2]], slot=r % 2)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / reps
     s = eng.stream
     eng.launch(b, s, capture=True)            # builds + captures any invalidated program
     for _ in range(warm):
@@ -106,6 +118,7 @@ def main(argv=None) -> int:
     ap.add_argument("--model", default="xception")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--lanes", type=int, default=2)
+    ap.add_argument("--stages", default=None, metavar="STEP", help="tune a stage-pipelined engine cut after STEP")
     ap.add_argument("--passes", type=int, default=1)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--start", default=None, help="starting table (default: the committed table)")
@@ -116,13 +129,17 @@ def main(argv=None) -> int:
     dev = torch.device("cuda", 0)
     info = registry.get(a.model)
     params = info.init_params(0)
-    if a.lanes > 1:
+    if a.stages:
+        from .stages import StagePipe
+        eng = StagePipe(info.engine(params, a.batch, dev), a.stages)
+        eng.add_input_slots(2)
+    elif a.lanes > 1:
         from .lanes import LaneGroup
         eng = LaneGroup(info, params, a.batch, dev, a.lanes)
     else:
         eng = info.engine(params, a.batch, dev)
     tname = info.tuning or a.model
-    start = Path(a.start) if a.start else tuning_path(tname, a.batch, a.lanes)
+    start = Path(a.start) if a.start else tuning_path(tname, a.batch, 1 if a.stages else a.lanes)
     if not start.exists():
         start = tuning_path(tname, a.batch)
     eng.load_tuning(start)

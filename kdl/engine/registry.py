@@ -20,6 +20,7 @@ class ModelInfo:
     oracle: Callable          # (params, uint8 NHWC) -> fp32 logits
     dtype: str = "bf16"       # compute dtype of the engine (bench.py's "dtype" field)
     tuning: str = ""          # tuning-table family name when it differs from ``name``
+    stage_cut: str = ""       # default stage-pipeline cut (stages.py) for bench / serving; "" = lanes
 
 
 def _xception():
@@ -30,7 +31,8 @@ def _xception():
                      lambda seed=0: X.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: XceptionEngine(p, max_batch=max_batch, device=device,
                                                                        in_kind="u8", **kw),
-                     lambda p, x: X.xception_forward(p, x.float() / 127.5 - 1.0))
+                     lambda p, x: X.xception_forward(p, x.float() / 127.5 - 1.0),
+                     stage_cut="block7_sepconv1")
 
 
 def _resnet50(dtype: str = "fp16"):

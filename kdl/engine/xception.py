@@ -179,6 +179,7 @@ class XceptionEngine(EngineBase):
                 H, W, _, _ = st.geom
                 n = max(n, B * H * W * st.layer.cin_pad)
         self.dwtmp = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        self.bufs["__dwtmp"] = self.dwtmp     # by name, so stages.py can give each stage its own
 
     # ------------------------------------------------------------------ programs
     def _ptr(self, name: str) -> int:
@@ -186,7 +187,13 @@ class XceptionEngine(EngineBase):
             return self.input_ptr()
         if name == "logits":
             return self.output_ptr()
-        return _lib.ptr(self.bufs[name])
+        return _lib.ptr(self.bufs[self._remap.get(name, name)])
+
+    def alias_buffer(self, name: str, alias: str) -> None:
+        """Second copy of an activation buffer (``stages.StagePipe`` double-buffers the
+        stage boundary so stage 1 of batch i+1 and stage 2 of batch i can overlap)."""
+        if alias not in self.bufs:
+            self.bufs[alias] = torch.zeros_like(self.bufs[name])
 
     def _emit(self, prog, step: Step, b: int) -> None:
         H, W, OH, OW = step.geom
@@ -215,7 +222,7 @@ class XceptionEngine(EngineBase):
         H, W, OH, OW = step.geom
         step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
                         res=self._ptr(step.res) if step.res else None, ldx=self.shapes[step.src][2],
-                        ldr=self.shapes[step.res][2] if step.res else None, tmp=_lib.ptr(self.dwtmp),
+                        ldr=self.shapes[step.res][2] if step.res else None, tmp=self._ptr("__dwtmp"),
                         split=split, cfg=cfg)
 
     def flops_per_image(self) -> float:

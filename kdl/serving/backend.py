@@ -311,11 +311,23 @@ class GPUExecutor(_Executor):
                 self.lanes.load_tuning(tp)
             self.lanes.program(bs[-1], capture=True)
             self.lanes.launch(bs[-1])
+        # stage pipelining of full top-bucket batches (kdl/engine/stages.py): stage 1 of
+        # batch n+1 overlaps stage 2 of batch n. Default: the family's cut (Xception:
+        # after block7_sepconv1) unless lanes were asked for; KDL_STAGES=none disables.
+        self.pipe = None
+        cut = self.engine_kwargs.get("stages", os.environ.get("KDL_STAGES", ""))
+        if not cut and src.family in ("xception",):
+            cut = registry.get(src.family).stage_cut
+        if cut and cut != "none" and self.lanes is None and hasattr(self.engine, "alias_buffer"):
+            from ..engine.stages import StagePipe
+            self.pipe = StagePipe(make(bs[-1]), cut)
+            if tp.exists():
+                self.pipe.load_tuning(tp)
         # pipelining depth (batches in flight per GPU): staging / output slots, each with
         # its own captured graphs (engine input slots), so the host can form batch n+1
         # while batch n runs
         self.depth = max(1, int(self.engine_kwargs.get("depth", os.environ.get("KDL_EXEC_DEPTH", "2"))))
-        for e in (self.engine, self.lanes):
+        for e in (self.engine, self.lanes, self.pipe):
             if e is not None:
                 e.add_input_slots(self.depth)
         dt = torch.uint8 if in_kind == "u8" else torch.float32
@@ -331,9 +343,10 @@ class GPUExecutor(_Executor):
             for bk in bs:
                 self.engine.program(bk, capture=True, slot=slot)
                 self.engine.launch(bk, slot=slot)
-            if self.lanes is not None:
-                self.lanes.program(bs[-1], capture=True, slot=slot)
-                self.lanes.launch(bs[-1], slot=slot)
+            for big in (self.lanes, self.pipe):
+                if big is not None:
+                    big.program(bs[-1], capture=True, slot=slot)
+                    big.launch(bs[-1], slot=slot)
         torch.cuda.synchronize(self.device)
 
     def staging_ptr(self, slot: int = 0) -> int:
@@ -343,17 +356,23 @@ class GPUExecutor(_Executor):
         """H2D on the copy stream (no device-side wait on a graph event: the slot's
         previous batch was completed on the host before the batcher refilled it),
         then the bucket's graph and the logits D2H on the engine stream."""
-        e = self.lanes if self.lanes is not None and bucket == self.lanes.max_batch else self.engine
+        big = self.lanes or self.pipe
+        e = big if big is not None and bucket == big.max_batch else self.engine
         C = self._rt
         stg, inp = self.staging[slot], e.inputs[slot]
         nbytes = bucket * stg[0].numel() * stg.element_size()
         C.memcpy_async(inp.data_ptr(), stg.data_ptr(), nbytes, 1, self.copy_stream.cuda_stream)
         self.h2d_done[slot].record(self.copy_stream)
-        e.stream.wait_event(self.h2d_done[slot])
-        e.launch(bucket, e.stream, slot=slot)
+        if e is self.pipe:                    # free-running stages; logits final on stage 2's stream
+            e.launch_async(bucket, [self.h2d_done[slot]], [self.done[slot]], slot=slot)
+            out_stream = e.streams[1]
+        else:
+            e.stream.wait_event(self.h2d_done[slot])
+            e.launch(bucket, e.stream, slot=slot)
+            out_stream = e.stream
         lg = e.slot_logits(slot)
-        C.memcpy_async(self.out[slot].data_ptr(), lg.data_ptr(), bucket * lg.shape[1] * 4, 2, e.stream.cuda_stream)
-        self.done[slot].record(e.stream)
+        C.memcpy_async(self.out[slot].data_ptr(), lg.data_ptr(), bucket * lg.shape[1] * 4, 2, out_stream.cuda_stream)
+        self.done[slot].record(out_stream)
         return slot
 
     def complete(self, slot: int) -> int:

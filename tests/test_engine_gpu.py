@@ -80,3 +80,42 @@ def test_lane_group_matches_single_engine(xparams):
     out = lanes.slot_logits(1).cpu()
     assert torch.allclose(out, ref, rtol=1e-3, atol=1e-3), (out, ref)
     assert lanes.slot_logits(0).abs().sum().item() == 0.0   # slot 0 untouched
+
+
+@pytest.mark.parametrize("cut", ["block4_pool", "block7_sepconv1"])
+def test_stage_pipe_matches_single_engine(xparams, cut):
+    """Stage pipelining (kdl/engine/stages.py): four batches in flight on two slots,
+    stage 1 of batch i+1 overlapping stage 2 of batch i with parity-double-buffered
+    boundary buffers (a mid-block cut also double-buffers the block's residual input)
+    and per-stage depthwise scratch (split separable convs in both stages), reproduce
+    the plain engine's logits batch for batch."""
+    from kdl.engine.stages import StagePipe
+    from kdl.engine.xception import XceptionEngine
+    single = XceptionEngine(xparams, max_batch=4)
+    table = single.tuning()
+    for name in ("block4_sepconv1", "block13_sepconv2"):    # split lowering in each stage
+        table[name] = [1, table[name][1] if table[name][1] < 64 else 16]
+    single.apply_tuning(table)
+    assert single.tuning()["block4_sepconv1"][0] == 1 and single.tuning()["block13_sepconv2"][0] == 1
+    pipe = StagePipe(XceptionEngine(xparams, max_batch=4), cut)
+    pipe.apply_tuning(table)
+    slots = pipe.add_input_slots(2)
+    gen = torch.Generator().manual_seed(21)
+    imgs = [torch.randint(0, 256, (4, 299, 299, 3), generator=gen, dtype=torch.uint8) for _ in range(4)]
+    refs = [single.forward(x.cuda()).cpu() for x in imgs]
+    outs = []
+    done = [torch.cuda.Event() for _ in range(2)]
+    for i, x in enumerate(imgs):
+        j = i % 2
+        if i >= 2:                                  # slot j free again: batch i-2 finished
+            done[j].synchronize()
+            outs.append(pipe.slot_logits(j).cpu())
+        slots[j].copy_(x.cuda())                   # current stream; no device-wide sync, so
+        ready = torch.cuda.Event()                 # the stages of consecutive batches overlap
+        ready.record()
+        pipe.launch_async(4, [ready], [done[j]], slot=j)
+    for i in (2, 3):
+        done[i % 2].synchronize()
+        outs.append(pipe.slot_logits(i % 2).cpu())
+    for o, r in zip(outs, refs):
+        assert torch.allclose(o, r, rtol=1e-3, atol=1e-3), (o, r)
