@@ -151,7 +151,9 @@ def main(argv=None) -> int:
     s = eng.stream                          # compute: graph replays
     cs = torch.cuda.Stream(device=dev)      # ingress H2D
     ms = torch.cuda.Stream(device=dev) if world > 1 else None   # RCCL scatter / gather + egress D2H
-    ds = torch.cuda.Stream(device=dev) if world == 1 else None  # egress D2H (one GPU)
+    # egress D2H (one GPU); stage-pipelined engines copy out on their last stage's stream
+    # instead, so compute stages + H2D + egress stay within GPU_MAX_HW_QUEUES (4)
+    ds = torch.cuda.Stream(device=dev) if world == 1 and not a.stages else None
     E = lambda: [torch.cuda.Event() for _ in range(NS)]  # noqa: E731
     ready, scattered, drained = E(), E(), E()
     # free[j]: slot j's input and logits are final -- one event per lane (free-running
@@ -224,13 +226,15 @@ def main(argv=None) -> int:
                 if timed:
                     t_out[i].record(ms)
             return
-        with torch.cuda.stream(ds):
-            for f in free[j]:
-                ds.wait_event(f)
-            d2h(out_host[j], out, ds)
-            drained[j].record(ds)
+        es = eng.out_stream if a.stages else ds     # stages: D2H behind the last stage on its stream
+        with torch.cuda.stream(es):
+            if es is ds:
+                for f in free[j]:
+                    ds.wait_event(f)
+            d2h(out_host[j], out, es)
+            drained[j].record(es)
             if timed:
-                t_out[i].record(ds)
+                t_out[i].record(es)
 
     def d2h(dst, src, stream):
         if a.copy == "raw":
@@ -331,7 +335,7 @@ def main(argv=None) -> int:
                        "global_batch": n_global, "seq_len": None, "image_size": S,
                        "per_gpu_batch": B, "parallelism": f"dp{world}",
                        "ingress": a.ingress, "hipgraph": use_graph, "lanes": a.lanes,
-                       **({"stages": f"2 (cut after {a.stages})"} if a.stages else {})},
+                       **({"stages": f"{len(eng.ranges)} (cut after {a.stages})"} if a.stages else {})},
         }
         print(json.dumps(res), flush=True)
         print(f"host issue time {t_issue * 1e3 / a.steps:.3f} ms/step (ingress {tt[0] * 1e3 / a.steps:.3f}, "

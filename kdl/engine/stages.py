@@ -30,42 +30,61 @@ import torch
 class StagePipe:
     pipelined = True          # consecutive batches overlap (graph_tune times it free-running)
 
-    def __init__(self, engine, split_after: str):
+    def __init__(self, engine, split_after):
+        """``split_after``: one step name (two stages) or a comma-separated list / list of
+        names (one stage per segment, one HIP stream each)."""
         self.engine = engine
         self.device = engine.device
         self.max_batch = engine.max_batch
+        cuts = split_after.split(",") if isinstance(split_after, str) else list(split_after)
         names = [s.name for s in engine.steps]
-        if split_after not in names:
-            raise ValueError(f"no step {split_after!r}; steps: {names}")
-        self.cut = names.index(split_after) + 1
-        st1, st2 = engine.steps[:self.cut], engine.steps[self.cut:]
-        # double-buffer (by batch parity) EVERY buffer stage 1 writes and stage 2 reads:
-        # the cut step's output and, inside a middle-flow block, the block input that the
-        # block's last separable conv adds back as its residual
-        written = {s.dst for s in st1}
-        read2 = {b for s in st2 for b in (s.src, s.res) if b}
-        self.boundary = sorted(written & read2 - {"input", "logits"})
+        for c in cuts:
+            if c not in names:
+                raise ValueError(f"no step {c!r}; steps: {names}")
+        bounds = [0] + sorted(names.index(c) + 1 for c in cuts) + [len(names)]
+        self.ranges = [(lo, hi) for lo, hi in zip(bounds, bounds[1:]) if hi > lo]
+        self.cut = self.ranges[0][1]
+        K = len(self.ranges)
+        stage_of = {}
+        for k, (lo, hi) in enumerate(self.ranges):
+            for st in engine.steps[lo:hi]:
+                stage_of[id(st)] = k
+        # a buffer written in stage a and read in a later stage b crosses a stage boundary:
+        # double-buffer it by batch parity; stage a of batch i+2 then waits for the last
+        # such reader of batch i before overwriting copy i % 2
+        writer, last_reader = {}, {}
+        for st in engine.steps:
+            k = stage_of[id(st)]
+            for b in (st.src, st.res):
+                if b and b in writer and writer[b] < k:
+                    last_reader[b] = max(last_reader.get(b, k), k)
+            if st.dst:
+                writer[st.dst] = k
+        self.boundary = sorted(b for b in last_reader if b not in ("input", "logits"))
         for b in self.boundary:
             engine.alias_buffer(b, b + "#1")
-        # stage-private scratch: the split (dw kernel + GEMM) separable convs of both stages
-        # would otherwise share one depthwise scratch buffer while running concurrently
-        engine.alias_buffer("__dwtmp", "__dwtmp#2")
-        self.remaps = [({}, {"__dwtmp": "__dwtmp#2"}),
-                       ({b: b + "#1" for b in self.boundary},
-                        {**{b: b + "#1" for b in self.boundary}, "__dwtmp": "__dwtmp#2"})]
-        self.streams = [engine.stream, torch.cuda.Stream(device=self.device)]
+        self.wait_for = [max([last_reader[b] for b in self.boundary if writer[b] == k] or [k]) for k in range(K)]
+        # stage-private scratch (the split separable convs' depthwise output buffer)
+        for k in range(1, K):
+            engine.alias_buffer("__dwtmp", f"__dwtmp#{k}")
+        self.remaps = [[{**({b: b + "#1" for b in self.boundary} if p else {}),
+                         **({"__dwtmp": f"__dwtmp#{k}"} if k else {})} for k in range(K)] for p in (0, 1)]
+        self.streams = [engine.stream] + [torch.cuda.Stream(device=self.device) for _ in range(K - 1)]
         self.stream = self.streams[0]
-        self.s1_done = [torch.cuda.Event() for _ in range(2)]
-        self.s2_done = [torch.cuda.Event() for _ in range(2)]
+        self.done = [[torch.cuda.Event() for _ in range(K)] for _ in range(2)]   # [parity][stage]
         self._fork = torch.cuda.Event()
-        for e in self.s1_done + self.s2_done:     # "done" before the first batch
+        for e in self.done[0] + self.done[1]:     # "done" before the first batch
             e.record(self.streams[0])
         self._n = 0                               # batches issued (parity of the next one)
-        self.inputs = engine.inputs
-        self.outputs = engine.outputs
         engine.add_input_slots(1)
+        self.inputs, self.outputs = engine.inputs, engine.outputs
         self.inp, self.logits = engine.inputs[0], engine.outputs[0]
         self.classes = self.logits.shape[1]
+
+    @property
+    def out_stream(self) -> torch.cuda.Stream:
+        """Stream on which the logits become final (the last stage's)."""
+        return self.streams[-1]
 
     # ---------------------------------------------------------------- tuning (engine's table)
     def load_tuning(self, path) -> None:
@@ -103,31 +122,33 @@ class StagePipe:
 
     # ---------------------------------------------------------------- execution
     def _progs(self, b: int, capture: bool, slot: int, parity: int):
-        e, (rm1, rm2) = self.engine, self.remaps[parity]
-        return (e.program_range(b, 0, self.cut, capture, slot, rm1),
-                e.program_range(b, self.cut, len(e.steps), capture, slot, rm2))
+        e = self.engine
+        return [e.program_range(b, lo, hi, capture, slot, self.remaps[parity][k])
+                for k, (lo, hi) in enumerate(self.ranges)]
 
     def program(self, b: int, capture: bool = True, slot: int = 0):
         return [self._progs(b, capture, slot, p) for p in (0, 1)]
 
     def launch_async(self, b: int, wait: list, done: list, capture: bool = True, slot: int = 0) -> None:
-        """Stage 1 waits on ``wait`` (input ready, logits drained) and on stage 2 of the
-        batch two back (boundary reuse); stage 2 waits on stage 1; ``done[0]`` fires when
-        the logits of slot ``slot`` are final."""
+        """Stage 0 waits on ``wait`` (input ready, logits drained); stage k waits on stage
+        k-1 of this batch and on the last later-stage reader of its double-buffered
+        outputs two batches back; ``done[0]`` fires when the logits of ``slot`` are final."""
         assert b == self.max_batch
         p = self._n & 1
         self._n += 1
-        p1, p2 = self._progs(b, capture, slot, p)
-        s1, s2 = self.streams
-        for w in wait:
-            s1.wait_event(w)
-        s1.wait_event(self.s2_done[p])
-        p1.launch(int(s1.cuda_stream))
-        self.s1_done[p].record(s1)
-        s2.wait_event(self.s1_done[p])
-        p2.launch(int(s2.cuda_stream))
-        self.s2_done[p].record(s2)
-        done[0].record(s2)
+        progs = self._progs(b, capture, slot, p)
+        ev = self.done[p]
+        for k, (prog, st) in enumerate(zip(progs, self.streams)):
+            if k == 0:
+                for w in wait:
+                    st.wait_event(w)
+            else:
+                st.wait_event(ev[k - 1])
+            if self.wait_for[k] > k:
+                st.wait_event(ev[self.wait_for[k]])   # recorded by batch i-2: its reader is done
+            prog.launch(int(st.cuda_stream))
+            ev[k].record(st)
+        done[0].record(self.streams[-1])
 
     def launch(self, b: int, stream: torch.cuda.Stream | None = None, capture: bool = True,
                slot: int = 0) -> None:

@@ -365,7 +365,7 @@ class GPUExecutor(_Executor):
         self.h2d_done[slot].record(self.copy_stream)
         if e is self.pipe:                    # free-running stages; logits final on stage 2's stream
             e.launch_async(bucket, [self.h2d_done[slot]], [self.done[slot]], slot=slot)
-            out_stream = e.streams[1]
+            out_stream = e.out_stream
         else:
             e.stream.wait_event(self.h2d_done[slot])
             e.launch(bucket, e.stream, slot=slot)
