@@ -104,16 +104,27 @@ class EngineBase:
         self.programs[key] = prog
         return prog
 
+    def alias_buffer(self, name: str, alias: str) -> None:
+        """Another physical copy of an activation buffer (``stages.StagePipe`` gives each
+        pipeline stage / batch parity its own copy of the buffers it shares)."""
+        if alias not in self.bufs:
+            self.bufs[alias] = torch.zeros_like(self.bufs[name])
+
     def program_range(self, b: int, lo: int, hi: int, capture: bool = True, slot: int = 0,
-                      remap: dict | None = None):
-        """Program of steps[lo:hi] only, with buffer names remapped (``stages.py``)."""
-        key = (b, capture, slot, lo, hi, tuple(sorted((remap or {}).items())))
+                      remap=None):
+        """Program of steps[lo:hi] only, with buffer names remapped (``stages.py``):
+        ``remap`` is one dict for all steps or a list with one dict per step."""
+        n = hi - lo
+        maps = list(remap) if isinstance(remap, (list, tuple)) else [dict(remap or {})] * n
+        assert len(maps) == n
+        key = (b, capture, slot, lo, hi, tuple(tuple(sorted(m.items())) for m in maps))
         if key in self.programs:
             return self.programs[key]
         prog = _lib.lib().Program()
-        self._slot, self._remap = slot, dict(remap or {})
+        self._slot = slot
         try:
-            for step in self.steps[lo:hi]:
+            for step, m in zip(self.steps[lo:hi], maps):
+                self._remap = m
                 self._emit(prog, step, b)
         finally:
             self._slot, self._remap = 0, {}

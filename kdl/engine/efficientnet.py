@@ -94,9 +94,11 @@ class EfficientNetEngine(EngineBase):
                                    p[f"{se}.fc1.bias"].float().to(dev),
                                    p[f"{se}.fc2.weight"].reshape(ce, blk.csq).t().float().contiguous().to(dev),
                                    p[f"{se}.fc2.bias"].float().to(dev))
-            self.steps.append(Step("se", f"{blk.prefix}.se", geom=(H, H, oh, oh),
+            self.steps.append(Step("se", f"{blk.prefix}.se", src="pool", dst="scale", geom=(H, H, oh, oh),
                                    extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
-            self.steps.append(Step("chscale", f"{blk.prefix}.scale", dst="D", geom=(oh, oh, oh, oh), extra=dict(C=ce)))
+            # in place on D (src == dst); reads the SE scales
+            self.steps.append(Step("chscale", f"{blk.prefix}.scale", src="D", dst="D", res="scale",
+                                   geom=(oh, oh, oh, oh), extra=dict(C=ce)))
             ping ^= 1
             out = f"X{ping}"
             lay = self._pw(n["project"], p, f"{n['project']}.0.weight", f"{n['project']}.1", ce, blk.cout, 0)
@@ -107,12 +109,12 @@ class EfficientNetEngine(EngineBase):
         lay = self._pw("features.8", p, "features.8.0.weight", "features.8.1", E.blocks()[-1].cout, E.HEAD, 4)
         self.steps.append(Step("conv", lay.name, lay, cur, "E", geom=(H, H, H, H), extra=dict(ldx=ldc)))
         self._need("E", H * H * E.HEAD)
-        self.steps.append(Step("gap", "avgpool", src="E", geom=(H, H, 1, 1)))
+        self.steps.append(Step("gap", "avgpool", src="E", dst="feat", geom=(H, H, 1, 1)))
         nf = (self.classes + 15) // 16
         self.fc_wp = pack_fragments(p["classifier.1.weight"].float(), nf, E.HEAD // 32).to(dev).contiguous()
         self.fc_nf = nf
         self.fc_b = p["classifier.1.bias"].float().to(dev)
-        self.steps.append(Step("fc", "classifier"))
+        self.steps.append(Step("fc", "classifier", src="feat", dst="logits"))
         # SE pooling partials: ntiles of each dw launch (host mirror of the kernel's tiling)
         C = _lib.lib()
         self.ntiles = {}
@@ -133,10 +135,19 @@ class EfficientNetEngine(EngineBase):
         self.pool = torch.zeros(B * self.pool_per_image, dtype=torch.float32, device=dev)
         self.scale = torch.zeros(B * max(b.cexp for b in E.blocks()), dtype=torch.float32, device=dev)
         self.feat = torch.zeros(((B + 15) // 16 * 16, E.HEAD), dtype=torch.bfloat16, device=dev)
+        # by name, so stages.py can version / privatise them like the activations
+        self.bufs.update(pool=self.pool, scale=self.scale, feat=self.feat)
         self.logits = torch.zeros((B, self.classes), dtype=torch.float32, device=dev)
 
     def _ptr(self, name: str) -> int:
-        return _lib.ptr(self.bufs[name])
+        if name == "logits":
+            return self.output_ptr()
+        return _lib.ptr(self.bufs[self._remap.get(name, name)])
+
+    def scratch_buffers(self) -> list[str]:
+        """SE partial pools (written by the dw kernel, not a step dst) and scales: used
+        within one block, so each pipeline stage gets its own (stages.py)."""
+        return ["pool", "scale"]
 
     def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
         H, W, OH, OW = step.geom
@@ -161,23 +172,23 @@ class EfficientNetEngine(EngineBase):
             w1 = self.se[step.extra["blk"]][0]
             K = step.extra["K"]
             prog.add_dwk(step.name, dict(x=self._ptr(step.src), w=_lib.ptr(w), bias=_lib.ptr(bias),
-                                         y=self._ptr("D"), pool=_lib.ptr(self.pool), w1=_lib.ptr(w1),
+                                         y=self._ptr("D"), pool=self._ptr("pool"), w1=_lib.ptr(w1),
                                          Cs=step.extra["Cs"], B=b, H=H, W=W, C=step.extra["C"], OH=OH, OW=OW,
                                          K=K, S=step.extra["S"], pad=(K - 1) // 2, act=2))
         elif step.kind == "se":
             _, b1, w2t, b2 = self.se[step.extra["blk"]]
-            prog.add_se(step.name, dict(pool=_lib.ptr(self.pool), b1=_lib.ptr(b1),
-                                        w2t=_lib.ptr(w2t), b2=_lib.ptr(b2), scale=_lib.ptr(self.scale), B=b,
+            prog.add_se(step.name, dict(pool=self._ptr("pool"), b1=_lib.ptr(b1),
+                                        w2t=_lib.ptr(w2t), b2=_lib.ptr(b2), scale=self._ptr("scale"), B=b,
                                         ntiles=self.ntiles[step.extra["blk"]], HW=OH * OW, C=step.extra["C"],
                                         Cs=step.extra["Cs"]))
         elif step.kind == "chscale":
-            prog.add_chscale(step.name, dict(y=self._ptr("D"), scale=_lib.ptr(self.scale), B=b, HW=OH * OW,
+            prog.add_chscale(step.name, dict(y=self._ptr("D"), scale=self._ptr("scale"), B=b, HW=OH * OW,
                                              C=step.extra["C"]))
         elif step.kind == "gap":
-            prog.add_gap(step.name, dict(x=self._ptr("E"), y=None, yb=_lib.ptr(self.feat), B=b, HW=H * W,
+            prog.add_gap(step.name, dict(x=self._ptr("E"), y=None, yb=self._ptr("feat"), B=b, HW=H * W,
                                          ldx=E.HEAD, F=E.HEAD))
         elif step.kind == "fc":
-            prog.add_fc_mfma(step.name, dict(xb=_lib.ptr(self.feat), wp=_lib.ptr(self.fc_wp),
+            prog.add_fc_mfma(step.name, dict(xb=self._ptr("feat"), wp=_lib.ptr(self.fc_wp),
                                              bias=_lib.ptr(self.fc_b), out=self.output_ptr(), B=b, F=E.HEAD,
                                              N=self.classes, NF=self.fc_nf, relu=0))
         else:  # pragma: no cover

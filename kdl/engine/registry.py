@@ -45,7 +45,7 @@ def _resnet50(dtype: str = "fp16"):
                      lambda seed=0: R.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: ResNetEngine(p, max_batch=max_batch, device=device,
                                                                      dtype=dtype, **kw),
-                     R.resnet_forward, dtype=dtype, tuning="resnet50")
+                     R.resnet_forward, dtype=dtype, tuning="resnet50", stage_cut="layer3.1.conv3")
 
 
 def _vit_b16():
@@ -66,7 +66,7 @@ def _efficientnet_b7():
                      lambda seed=0: E.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: EfficientNetEngine(p, max_batch=max_batch, device=device,
                                                                            **kw),
-                     E.efficientnet_forward)
+                     E.efficientnet_forward, stage_cut="features.4.9.block.3")
 
 
 def _vit_b16_fp8():

@@ -126,6 +126,7 @@ class ResNetEngine(EngineBase):
             n = B * (h + 2 * border) * (w + 2 * border) * c
             self.bufs[name] = torch.zeros(n, dtype=self.dtype, device=dev)   # borders stay 0
         self.feat = torch.zeros(((B + 15) // 16 * 16, 2048), dtype=self.dtype, device=dev)
+        self.bufs["feat"] = self.feat
         self.logits = torch.zeros((B, self.classes), dtype=torch.float32, device=dev)
 
     # ------------------------------------------------------------------ emission
@@ -134,9 +135,10 @@ class ResNetEngine(EngineBase):
             return self.input_ptr()
         if name == "logits":
             return self.output_ptr()
-        if name == "feat":
-            return _lib.ptr(self.feat)
-        return _lib.ptr(self.bufs[name])
+        return _lib.ptr(self.bufs[self._remap.get(name, name)])
+
+    def scratch_buffers(self) -> list[str]:
+        return []
 
     def _ld(self, name: str) -> int:
         return self.shapes[name][2]

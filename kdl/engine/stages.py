@@ -11,11 +11,13 @@ compete for the same resource at the same time; two stages of DIFFERENT layers
 can fill each other's gaps. Each stage runs the full batch, so every kernel keeps
 the b32 tile table.
 
-Every buffer written by stage 1 and read by stage 2 (the cut step's output, and
-inside a middle-flow block also the block input that comes back as the residual)
-is double-buffered by batch parity: stage 1 of batch i+2 may overwrite copy
-i % 2 only after stage 2 of batch i has read it (a device-side event wait on the
-stage-1 stream). Scratch buffers are per stage.
+Buffers are renamed per version (SSA over the step list): a version that crosses
+a cut (the cut step's output; inside a middle-flow block also the block input that
+comes back as the residual) is double-buffered by batch parity, and its writer
+stage of batch i+2 waits for its last reader stage of batch i (a device-side
+event wait); versions used inside one stage and the engine's scratch buffers get
+stage-private copies, since the stages run concurrently (ResNet reuses its
+per-stage pad / mid / ping-pong buffers across blocks).
 
 Interface: like an engine for ``bench.py`` / the serving executor (input slots,
 per-slot logits, ``launch`` joins into the caller's stream) plus
@@ -45,30 +47,63 @@ class StagePipe:
         self.ranges = [(lo, hi) for lo, hi in zip(bounds, bounds[1:]) if hi > lo]
         self.cut = self.ranges[0][1]
         K = len(self.ranges)
-        stage_of = {}
-        for k, (lo, hi) in enumerate(self.ranges):
-            for st in engine.steps[lo:hi]:
-                stage_of[id(st)] = k
-        # a buffer written in stage a and read in a later stage b crosses a stage boundary:
-        # double-buffer it by batch parity; stage a of batch i+2 then waits for the last
-        # such reader of batch i before overwriting copy i % 2
-        writer, last_reader = {}, {}
-        for st in engine.steps:
-            k = stage_of[id(st)]
-            for b in (st.src, st.res):
-                if b and b in writer and writer[b] < k:
-                    last_reader[b] = max(last_reader.get(b, k), k)
-            if st.dst:
-                writer[st.dst] = k
-        self.boundary = sorted(b for b in last_reader if b not in ("input", "logits"))
-        for b in self.boundary:
-            engine.alias_buffer(b, b + "#1")
-        self.wait_for = [max([last_reader[b] for b in self.boundary if writer[b] == k] or [k]) for k in range(K)]
-        # stage-private scratch (the split separable convs' depthwise output buffer)
-        for k in range(1, K):
-            engine.alias_buffer("__dwtmp", f"__dwtmp#{k}")
-        self.remaps = [[{**({b: b + "#1" for b in self.boundary} if p else {}),
-                         **({"__dwtmp": f"__dwtmp#{k}"} if k else {})} for k in range(K)] for p in (0, 1)]
+        steps = engine.steps
+        stage = [k for k, (lo, hi) in enumerate(self.ranges) for _ in range(lo, hi)]
+        # Buffer versions (SSA over the sequential step list): a read of X at step i sees
+        # the last write of X before i. A version read only inside its writer's stage a
+        # lives in a stage-private copy (X in stage 0, X#s<a> otherwise: stages run
+        # concurrently); a version read by a later stage is double-buffered by batch
+        # parity (X#x<a>p0 / X#x<a>p1), and stage a of batch i+2 waits for its last
+        # reader stage of batch i before overwriting it.
+        last_write: dict[str, int] = {}
+        reads = []                               # per step: {name: writer step or -1}
+        readers: dict[int, int] = {}             # writer step -> max reader stage
+        for i, st in enumerate(steps):
+            r = {}
+            for nm in (st.src, st.res):
+                if nm and nm not in ("input", "logits"):
+                    w = last_write.get(nm, -1)
+                    r[nm] = w
+                    if w >= 0:
+                        readers[w] = max(readers.get(w, stage[w]), stage[i])
+            reads.append(r)
+            if st.dst and st.dst not in ("input", "logits"):
+                last_write[st.dst] = i
+
+        touched: dict[str, set] = {}             # stages that read or write each name
+        for i, st in enumerate(steps):
+            for nm in (st.src, st.res, st.dst):
+                if nm:
+                    touched.setdefault(nm, set()).add(stage[i])
+
+        def phys(nm: str, w: int, p: int) -> str:
+            a = stage[w]
+            if readers.get(w, a) > a:
+                return f"{nm}#x{a}p{p}"
+            return nm if a == 0 or len(touched[nm]) == 1 else f"{nm}#s{a}"
+
+        self.remaps = [[], []]
+        self.wait_for = list(range(K))
+        self.boundary = set()
+        for i, st in enumerate(steps):
+            for p in (0, 1):
+                m = {nm: phys(nm, w, p) for nm, w in reads[i].items() if w >= 0}
+                if st.dst and st.dst not in ("input", "logits"):
+                    ph = phys(st.dst, i, p)
+                    if st.dst in m and m[st.dst] != ph:   # in-place step whose versions differ
+                        raise ValueError(f"in-place step {st.name}: a cut right after it is not supported")
+                    m[st.dst] = ph
+                for k_name in getattr(engine, "scratch_buffers", lambda: [])():
+                    if stage[i]:
+                        m[k_name] = f"{k_name}#s{stage[i]}"
+                for base, ph in m.items():
+                    if ph != base:
+                        engine.alias_buffer(base, ph)
+                self.remaps[p].append(m)
+            if st.dst and readers.get(i, stage[i]) > stage[i]:
+                self.boundary.add(st.dst)
+                self.wait_for[stage[i]] = max(self.wait_for[stage[i]], readers[i])
+        self.boundary = sorted(self.boundary)
         self.streams = [engine.stream] + [torch.cuda.Stream(device=self.device) for _ in range(K - 1)]
         self.stream = self.streams[0]
         self.done = [[torch.cuda.Event() for _ in range(K)] for _ in range(2)]   # [parity][stage]
@@ -123,8 +158,8 @@ class StagePipe:
     # ---------------------------------------------------------------- execution
     def _progs(self, b: int, capture: bool, slot: int, parity: int):
         e = self.engine
-        return [e.program_range(b, lo, hi, capture, slot, self.remaps[parity][k])
-                for k, (lo, hi) in enumerate(self.ranges)]
+        return [e.program_range(b, lo, hi, capture, slot, self.remaps[parity][lo:hi])
+                for lo, hi in self.ranges]
 
     def program(self, b: int, capture: bool = True, slot: int = 0):
         return [self._progs(b, capture, slot, p) for p in (0, 1)]

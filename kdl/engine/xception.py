@@ -189,11 +189,10 @@ class XceptionEngine(EngineBase):
             return self.output_ptr()
         return _lib.ptr(self.bufs[self._remap.get(name, name)])
 
-    def alias_buffer(self, name: str, alias: str) -> None:
-        """Second copy of an activation buffer (``stages.StagePipe`` double-buffers the
-        stage boundary so stage 1 of batch i+1 and stage 2 of batch i can overlap)."""
-        if alias not in self.bufs:
-            self.bufs[alias] = torch.zeros_like(self.bufs[name])
+
+    def scratch_buffers(self) -> list[str]:
+        """Buffers a step uses that are not its src / dst / res (stages.py privatises them)."""
+        return ["__dwtmp"]
 
     def _emit(self, prog, step: Step, b: int) -> None:
         H, W, OH, OW = step.geom

@@ -316,7 +316,7 @@ class GPUExecutor(_Executor):
         # after block7_sepconv1) unless lanes were asked for; KDL_STAGES=none disables.
         self.pipe = None
         cut = self.engine_kwargs.get("stages", os.environ.get("KDL_STAGES", ""))
-        if not cut and src.family in ("xception",):
+        if not cut:
             cut = registry.get(src.family).stage_cut
         if cut and cut != "none" and self.lanes is None and hasattr(self.engine, "alias_buffer"):
             from ..engine.stages import StagePipe

@@ -67,3 +67,36 @@ def test_efficientnet_engine_matches_oracle():
         # a plain torch bf16 forward of the same oracle measures cosine 0.945 / 0.980 on these two
         # images (55 blocks of bf16 drift); the fused engine keeps fp32 accumulators throughout
         assert cos.min() > 0.96, cos
+
+
+def test_efficientnet_stage_pipe_matches_engine():
+    """Stage pipelining of EfficientNet (kdl/engine/stages.py): both stages reuse the E / D /
+    X ping-pong buffers and the SE pool / scale scratch (stage-private copies), the
+    in-place channel scale keeps one version; four batches on two slots match the engine."""
+    from kdl.engine.efficientnet import EfficientNetEngine
+    from kdl.engine.stages import StagePipe
+    S = 256
+    p = E.init_params(seed=0, calib_size=S)
+    single = EfficientNetEngine(p, max_batch=2, device=DEV, size=S)
+    eng2 = EfficientNetEngine(p, max_batch=2, device=DEV, size=S)
+    projs = [s for s in eng2.steps if s.kind == "conv" and s.src == "D"]
+    pipe = StagePipe(eng2, projs[len(projs) // 2].name)
+    slots = pipe.add_input_slots(2)
+    gen = torch.Generator().manual_seed(12)
+    imgs = [torch.randint(0, 256, (2, S, S, 3), generator=gen, dtype=torch.uint8) for _ in range(4)]
+    refs = [single.forward(x.to(DEV)).cpu() for x in imgs]
+    outs, done = [], [torch.cuda.Event() for _ in range(2)]
+    for i, x in enumerate(imgs):
+        j = i % 2
+        if i >= 2:
+            done[j].synchronize()
+            outs.append(pipe.slot_logits(j).cpu())
+        slots[j].copy_(x.to(DEV))
+        ready = torch.cuda.Event()
+        ready.record()
+        pipe.launch_async(2, [ready], [done[j]], slot=j)
+    for i in (2, 3):
+        done[i % 2].synchronize()
+        outs.append(pipe.slot_logits(i % 2).cpu())
+    for o, r in zip(outs, refs):
+        assert torch.allclose(o, r, rtol=1e-3, atol=1e-3), (o - r).abs().max()

@@ -182,3 +182,34 @@ def test_fp16_gap_fc_and_pool():
     torch.cuda.synchronize()
     refp = F.max_pool2d(xp.float().permute(0, 3, 1, 2), 3, 2, padding=1).permute(0, 2, 3, 1)
     assert torch.equal(yp.view(2, OH, OH, Cc).float(), refp)
+
+
+def test_resnet_stage_pipe_matches_engine(rparams):
+    """Stage pipelining of ResNet-50 (kdl/engine/stages.py): a cut inside layer3 makes both
+    stages use the same per-stage pad / mid / ping-pong buffer names, which the version
+    renaming gives stage-private copies; four batches in flight on two slots match the
+    plain engine."""
+    from kdl.engine.resnet import ResNetEngine
+    from kdl.engine.stages import StagePipe
+    single = ResNetEngine(rparams, max_batch=4, device=DEV)
+    pipe = StagePipe(ResNetEngine(rparams, max_batch=4, device=DEV), "layer3.2.conv3")
+    pipe.apply_tuning(single.tuning())
+    slots = pipe.add_input_slots(2)
+    gen = torch.Generator().manual_seed(9)
+    imgs = [torch.randint(0, 256, (4, 224, 224, 3), generator=gen, dtype=torch.uint8) for _ in range(4)]
+    refs = [single.forward(x.to(DEV)).cpu() for x in imgs]
+    outs, done = [], [torch.cuda.Event() for _ in range(2)]
+    for i, x in enumerate(imgs):
+        j = i % 2
+        if i >= 2:
+            done[j].synchronize()
+            outs.append(pipe.slot_logits(j).cpu())
+        slots[j].copy_(x.to(DEV))
+        ready = torch.cuda.Event()
+        ready.record()
+        pipe.launch_async(4, [ready], [done[j]], slot=j)
+    for i in (2, 3):
+        done[i % 2].synchronize()
+        outs.append(pipe.slot_logits(i % 2).cpu())
+    for o, r in zip(outs, refs):
+        assert torch.allclose(o, r, rtol=1e-3, atol=1e-3), (o - r).abs().max()
