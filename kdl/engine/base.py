@@ -104,6 +104,11 @@ class EngineBase:
         self.programs[key] = prog
         return prog
 
+    def _wptr(self, name: str) -> int:
+        """Destination pointer of a step: a residual GEMM (res == dst) may write a different
+        physical copy than it reads (stages.py versioning puts that under ``name@w``)."""
+        return self._ptr(name + "@w") if (name + "@w") in self._remap else self._ptr(name)
+
     def alias_buffer(self, name: str, alias: str) -> None:
         """Another physical copy of an activation buffer (``stages.StagePipe`` gives each
         pipeline stage / batch parity its own copy of the buffers it shares)."""

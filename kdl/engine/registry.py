@@ -55,7 +55,7 @@ def _vit_b16():
                      "ViT-B/16 224x224 (torchvision layout, 86,567,656 params)",
                      lambda seed=0: V.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: ViTEngine(p, max_batch=max_batch, device=device, **kw),
-                     V.vit_forward)
+                     V.vit_forward, stage_cut="encoder.layers.encoder_layer_5.mlp.3")
 
 
 def _efficientnet_b7():
@@ -77,7 +77,8 @@ def _vit_b16_fp8():
                      lambda seed=0: V.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: ViTEngine(p, max_batch=max_batch, device=device, fp8=True,
                                                                   **kw),
-                     V.vit_forward, dtype="fp8-e4m3 linears / bf16 rest")
+                     V.vit_forward, dtype="fp8-e4m3 linears / bf16 rest",
+                     stage_cut="encoder.layers.encoder_layer_5.mlp.3")
 
 
 _FACTORIES = {"xception": _xception, "resnet50": _resnet50, "resnet50_bf16": lambda: _resnet50("bf16"),

@@ -90,13 +90,21 @@ class StagePipe:
                 m = {nm: phys(nm, w, p) for nm, w in reads[i].items() if w >= 0}
                 if st.dst and st.dst not in ("input", "logits"):
                     ph = phys(st.dst, i, p)
-                    if st.dst in m and m[st.dst] != ph:   # in-place step whose versions differ
+                    # a true in-place step (src == dst: one pointer, e.g. a channel scale) needs
+                    # both versions in one buffer; a residual GEMM with res == dst reads and
+                    # writes through separate pointers, so its versions may differ
+                    if st.src == st.dst and m.get(st.dst, ph) != ph:
                         raise ValueError(f"in-place step {st.name}: a cut right after it is not supported")
-                    m[st.dst] = ph
+                    if st.res == st.dst and st.src != st.dst:
+                        m = dict(m)
+                        m[st.dst + "@w"] = ph      # write pointer, see EngineBase._wptr
+                    else:
+                        m[st.dst] = ph
                 for k_name in getattr(engine, "scratch_buffers", lambda: [])():
                     if stage[i]:
                         m[k_name] = f"{k_name}#s{stage[i]}"
-                for base, ph in m.items():
+                for key, ph in m.items():
+                    base = key[:-2] if key.endswith("@w") else key
                     if ph != base:
                         engine.alias_buffer(base, ph)
                 self.remaps[p].append(m)

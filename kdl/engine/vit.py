@@ -76,7 +76,7 @@ class ViTEngine(EngineBase):
                                "patches", "X", extra=dict(kind="patch")))
         self.cls = p["class_token"].reshape(D).float().to(dev)
         self.pos = p["encoder.pos_embedding"].reshape(self.T, D).float().contiguous().to(dev)
-        self.steps.append(Step("embed", "embed", dst="X"))
+        self.steps.append(Step("embed", "embed", src="X", dst="X"))       # in place on the patch embeddings
         self.f8scale: dict[str, float] = {}
         for i in range(V.DEPTH):
             L = f"encoder.layers.encoder_layer_{i}"
@@ -144,7 +144,10 @@ class ViTEngine(EngineBase):
         self.logits = torch.zeros((B, self.classes), dtype=torch.float32, device=dev)
 
     def _ptr(self, name: str) -> int:
-        return _lib.ptr(self.bufs[name])
+        return _lib.ptr(self.bufs[self._remap.get(name, name)])
+
+    def scratch_buffers(self) -> list[str]:
+        return []
 
     def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
         if step.kind == "f8":
@@ -152,9 +155,9 @@ class ViTEngine(EngineBase):
             kw = dict(x8=self._ptr(step.src), M=b * self.T, res=self._ptr(step.res) if step.res else None,
                       ldy=self.ld[step.dst])
             if out_scale is not None:
-                kw.update(y8=self._ptr(step.dst), out_scale=out_scale)
+                kw.update(y8=self._wptr(step.dst), out_scale=out_scale)
             else:
-                kw.update(y=self._ptr(step.dst))
+                kw.update(y=self._wptr(step.dst))
             step.layer.emit(prog, cfg=cfg, **kw)
             return
         lay: ConvGemmLayer = step.layer
@@ -166,7 +169,7 @@ class ViTEngine(EngineBase):
             rows = b * self.T
             g = Geometry(1, 1, rows, 1, rows)
             opad = 0
-        lay.emit(prog, self._ptr(step.src), self._ptr(step.dst), g,
+        lay.emit(prog, self._ptr(step.src), self._wptr(step.dst), g,
                  res=self._ptr(step.res) if step.res else None, ldx=self.ld[step.src],
                  ldr=self.ld[step.res] if step.res else None, split=False, cfg=cfg, opad=opad)
 

@@ -94,3 +94,36 @@ def test_vit_engine_matches_oracle():
         cos = F.cosine_similarity(out, ref, dim=1)
         assert cos.min() > 0.99, cos
         assert _rel(out, ref) < 0.1
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_vit_stage_pipe_matches_engine(fp8):
+    """Stage pipelining of ViT-B/16 (kdl/engine/stages.py): the residual stream X is
+    updated by residual GEMMs (res == dst), so a cut between encoder layers hands X across
+    in a parity double-buffer and the first residual GEMM of stage 2 writes a stage-private
+    copy through a separate write pointer; four batches on two slots match the engine."""
+    from kdl.engine.stages import StagePipe
+    from kdl.engine.vit import ViTEngine
+    from kdl.models import vit as V
+    p = V.init_params(seed=0)
+    single = ViTEngine(p, max_batch=2, device="cuda", fp8=fp8)
+    pipe = StagePipe(ViTEngine(p, max_batch=2, device="cuda", fp8=fp8), "encoder.layers.encoder_layer_5.mlp.3")
+    slots = pipe.add_input_slots(2)
+    gen = torch.Generator().manual_seed(14)
+    imgs = [torch.randint(0, 256, (2, 224, 224, 3), generator=gen, dtype=torch.uint8) for _ in range(4)]
+    refs = [single.forward(x.cuda()).cpu() for x in imgs]
+    outs, done = [], [torch.cuda.Event() for _ in range(2)]
+    for i, x in enumerate(imgs):
+        j = i % 2
+        if i >= 2:
+            done[j].synchronize()
+            outs.append(pipe.slot_logits(j).cpu())
+        slots[j].copy_(x.cuda())
+        ready = torch.cuda.Event()
+        ready.record()
+        pipe.launch_async(2, [ready], [done[j]], slot=j)
+    for i in (2, 3):
+        done[i % 2].synchronize()
+        outs.append(pipe.slot_logits(i % 2).cpu())
+    for o, r in zip(outs, refs):
+        assert torch.allclose(o, r, rtol=1e-3, atol=1e-3), (o - r).abs().max()
