@@ -60,6 +60,7 @@ def main(argv=None) -> int:
                     help="stage-pipeline the forward (kdl/engine/stages.py): cut after this step; stage 1 "
                          "of batch i+1 overlaps stage 2 of batch i. Default: the model's cut (Xception: "
                          "block7_sepconv1, measured +10 %% over 2 lanes); 'none' = lanes")
+    ap.add_argument("--cu-share", default=None, help="stage CU shares, e.g. 0.6,0.4 (CU-masked stage streams)")
     ap.add_argument("--lanes-free", action="store_true",
                     help="free-running lane streams (LaneGroup.launch_async) instead of forking/joining "
                          "the lanes through one stream every batch (measured 1-3 %% slower on one GPU)")
@@ -106,7 +107,8 @@ def main(argv=None) -> int:
     if a.stages:
         from kdl.engine.stages import StagePipe
         assert a.lanes == 1, "--stages and --lanes > 1 are exclusive"
-        eng = StagePipe(info.engine(params, B, dev), a.stages)
+        eng = StagePipe(info.engine(params, B, dev), a.stages,
+                        cu_share=[float(f) for f in a.cu_share.split(",")] if a.cu_share else None)
     elif a.lanes > 1:
         from kdl.engine.lanes import LaneGroup
         eng = LaneGroup(info, params, B, dev, a.lanes)

@@ -355,7 +355,10 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(16, 8, 3, 5, 11)         \
   X(17, 12, 3, 6, 15)        \
   X(18, 6, 6, 5, 9)          \
-  X(19, 4, 6, 5, 8)
+  X(19, 4, 6, 5, 8)          \
+  X(20, 4, 3, 5, 8)          \
+  X(21, 4, 3, 6, 8)          \
+  X(22, 2, 6, 5, 8)
 
 // timing-ablation bits of the stamping ids: 1 no depthwise MFMA, 2 no pointwise MFMA,
 // 4 no band / weight LDS-DMA in the loop, 8 producers skip the depthwise entirely;

@@ -26,93 +26,148 @@ The reference has no equivalent (TF-Serving runs one session per batch).
 """
 from __future__ import annotations
 
+import ctypes
+from dataclasses import dataclass
+
 import torch
+
+
+def _cu_mask(k: int, shares: list, n_cu: int = 256) -> list[int]:
+    """32-bit mask words giving stage k its share of the CUs, interleaved over the CU
+    index (i mod 20 buckets) so every stage gets CUs on every XCD whatever the bit order."""
+    bounds, acc = [], 0.0
+    for f in shares:
+        acc += f
+        bounds.append(round(acc * 20))
+    lo = 0 if k == 0 else bounds[k - 1]
+    hi = bounds[k]
+    words = [0] * ((n_cu + 31) // 32)
+    for i in range(n_cu):
+        if lo <= i % 20 < hi:
+            words[i // 32] |= 1 << (i % 32)
+    return words
+
+
+def cu_masked_stream(device, words: list[int]) -> torch.cuda.ExternalStream:
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                  ctypes.POINTER(ctypes.c_uint32)]
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    ptr = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        err = hip.hipExtStreamCreateWithCUMask(ctypes.byref(ptr), len(words), arr)
+    if err != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({err})")
+    return torch.cuda.ExternalStream(ptr.value, device=device)
+
+
+@dataclass
+class StagePlan:
+    ranges: list            # [(lo, hi)] step ranges, one per stage
+    remaps: list            # [parity][step] -> {name: physical name} (name@w: write pointer)
+    boundary: list          # buffers with a version that crosses a cut
+    wait_for: list          # per stage: the last later stage it must wait for (parity reuse)
+    aliases: dict           # physical copy -> base buffer to allocate it like
+
+
+def plan_stages(steps, split_after, scratch=()) -> StagePlan:
+    """Pure analysis (no GPU): stage ranges and per-step buffer renaming for a cut list.
+
+    A read of X at step i sees the last write of X before i (SSA over the sequential
+    step list). A version read only inside its writer's stage a lives in a stage-private
+    copy (X in stage 0 or when no other stage touches X, X#s<a> otherwise: stages run
+    concurrently); a version read by a later stage is double-buffered by batch parity
+    (X#x<a>p0 / X#x<a>p1), and stage a then waits for its last reader stage two
+    batches back before overwriting it. ``scratch`` buffers get a copy per stage."""
+    cuts = split_after.split(",") if isinstance(split_after, str) else list(split_after)
+    names = [s.name for s in steps]
+    for c in cuts:
+        if c not in names:
+            raise ValueError(f"no step {c!r}; steps: {names}")
+    bounds = [0] + sorted(names.index(c) + 1 for c in cuts) + [len(names)]
+    ranges = [(lo, hi) for lo, hi in zip(bounds, bounds[1:]) if hi > lo]
+    K = len(ranges)
+    stage = [k for k, (lo, hi) in enumerate(ranges) for _ in range(lo, hi)]
+    last_write: dict = {}
+    reads = []                               # per step: {name: writer step or -1}
+    readers: dict = {}                       # writer step -> max reader stage
+    for i, st in enumerate(steps):
+        r = {}
+        for nm in (st.src, st.res):
+            if nm and nm not in ("input", "logits"):
+                w = last_write.get(nm, -1)
+                r[nm] = w
+                if w >= 0:
+                    readers[w] = max(readers.get(w, stage[w]), stage[i])
+        reads.append(r)
+        # a true in-place step (src == dst, one pointer: e.g. EfficientNet's channel scale)
+        # modifies the version it read instead of creating a new one
+        if st.dst and st.dst not in ("input", "logits") and st.src != st.dst:
+            last_write[st.dst] = i
+    touched: dict = {}                       # stages that read or write each name
+    for i, st in enumerate(steps):
+        for nm in (st.src, st.res, st.dst):
+            if nm:
+                touched.setdefault(nm, set()).add(stage[i])
+
+    def phys(nm: str, w: int, p: int) -> str:
+        a = stage[w]
+        if readers.get(w, a) > a:
+            return f"{nm}#x{a}p{p}"
+        return nm if a == 0 or len(touched[nm]) == 1 else f"{nm}#s{a}"
+
+    remaps, aliases, boundary = [[], []], {}, set()
+    wait_for = list(range(K))
+    for i, st in enumerate(steps):
+        for p in (0, 1):
+            m = {nm: phys(nm, w, p) for nm, w in reads[i].items() if w >= 0}
+            if st.dst and st.dst not in ("input", "logits") and st.src != st.dst:
+                ph = phys(st.dst, i, p)
+                # a residual GEMM with res == dst reads and writes through separate
+                # pointers, so the version it reads and the one it writes may differ
+                if st.res == st.dst:
+                    m[st.dst + "@w"] = ph      # write pointer, see EngineBase._wptr
+                else:
+                    m[st.dst] = ph
+            for k_name in scratch:
+                if stage[i]:
+                    m[k_name] = f"{k_name}#s{stage[i]}"
+            for key, ph in m.items():
+                base = key[:-2] if key.endswith("@w") else key
+                if ph != base:
+                    aliases[ph] = base
+            remaps[p].append(m)
+        if st.dst and readers.get(i, stage[i]) > stage[i]:
+            boundary.add(st.dst)
+            wait_for[stage[i]] = max(wait_for[stage[i]], readers[i])
+    return StagePlan(ranges, remaps, sorted(boundary), wait_for, aliases)
 
 
 class StagePipe:
     pipelined = True          # consecutive batches overlap (graph_tune times it free-running)
 
-    def __init__(self, engine, split_after):
+    def __init__(self, engine, split_after, cu_share: list | None = None):
         """``split_after``: one step name (two stages) or a comma-separated list / list of
-        names (one stage per segment, one HIP stream each)."""
+        names (one stage per segment, one HIP stream each). ``cu_share``: optional
+        fraction of the CUs per stage (CU-masked streams, hipExtStreamCreateWithCUMask),
+        so the stages run on disjoint CU sets; measured 20-65 % SLOWER than letting both
+        stages share every CU (profiles/stages_ab.txt), kept for experiments only."""
         self.engine = engine
         self.device = engine.device
         self.max_batch = engine.max_batch
-        cuts = split_after.split(",") if isinstance(split_after, str) else list(split_after)
-        names = [s.name for s in engine.steps]
-        for c in cuts:
-            if c not in names:
-                raise ValueError(f"no step {c!r}; steps: {names}")
-        bounds = [0] + sorted(names.index(c) + 1 for c in cuts) + [len(names)]
-        self.ranges = [(lo, hi) for lo, hi in zip(bounds, bounds[1:]) if hi > lo]
+        plan = plan_stages(engine.steps, split_after, getattr(engine, "scratch_buffers", lambda: [])())
+        for alias, base in plan.aliases.items():
+            engine.alias_buffer(base, alias)
+        self.ranges, self.remaps = plan.ranges, plan.remaps
+        self.boundary, self.wait_for = plan.boundary, plan.wait_for
         self.cut = self.ranges[0][1]
         K = len(self.ranges)
-        steps = engine.steps
-        stage = [k for k, (lo, hi) in enumerate(self.ranges) for _ in range(lo, hi)]
-        # Buffer versions (SSA over the sequential step list): a read of X at step i sees
-        # the last write of X before i. A version read only inside its writer's stage a
-        # lives in a stage-private copy (X in stage 0, X#s<a> otherwise: stages run
-        # concurrently); a version read by a later stage is double-buffered by batch
-        # parity (X#x<a>p0 / X#x<a>p1), and stage a of batch i+2 waits for its last
-        # reader stage of batch i before overwriting it.
-        last_write: dict[str, int] = {}
-        reads = []                               # per step: {name: writer step or -1}
-        readers: dict[int, int] = {}             # writer step -> max reader stage
-        for i, st in enumerate(steps):
-            r = {}
-            for nm in (st.src, st.res):
-                if nm and nm not in ("input", "logits"):
-                    w = last_write.get(nm, -1)
-                    r[nm] = w
-                    if w >= 0:
-                        readers[w] = max(readers.get(w, stage[w]), stage[i])
-            reads.append(r)
-            if st.dst and st.dst not in ("input", "logits"):
-                last_write[st.dst] = i
-
-        touched: dict[str, set] = {}             # stages that read or write each name
-        for i, st in enumerate(steps):
-            for nm in (st.src, st.res, st.dst):
-                if nm:
-                    touched.setdefault(nm, set()).add(stage[i])
-
-        def phys(nm: str, w: int, p: int) -> str:
-            a = stage[w]
-            if readers.get(w, a) > a:
-                return f"{nm}#x{a}p{p}"
-            return nm if a == 0 or len(touched[nm]) == 1 else f"{nm}#s{a}"
-
-        self.remaps = [[], []]
-        self.wait_for = list(range(K))
-        self.boundary = set()
-        for i, st in enumerate(steps):
-            for p in (0, 1):
-                m = {nm: phys(nm, w, p) for nm, w in reads[i].items() if w >= 0}
-                if st.dst and st.dst not in ("input", "logits"):
-                    ph = phys(st.dst, i, p)
-                    # a true in-place step (src == dst: one pointer, e.g. a channel scale) needs
-                    # both versions in one buffer; a residual GEMM with res == dst reads and
-                    # writes through separate pointers, so its versions may differ
-                    if st.src == st.dst and m.get(st.dst, ph) != ph:
-                        raise ValueError(f"in-place step {st.name}: a cut right after it is not supported")
-                    if st.res == st.dst and st.src != st.dst:
-                        m = dict(m)
-                        m[st.dst + "@w"] = ph      # write pointer, see EngineBase._wptr
-                    else:
-                        m[st.dst] = ph
-                for k_name in getattr(engine, "scratch_buffers", lambda: [])():
-                    if stage[i]:
-                        m[k_name] = f"{k_name}#s{stage[i]}"
-                for key, ph in m.items():
-                    base = key[:-2] if key.endswith("@w") else key
-                    if ph != base:
-                        engine.alias_buffer(base, ph)
-                self.remaps[p].append(m)
-            if st.dst and readers.get(i, stage[i]) > stage[i]:
-                self.boundary.add(st.dst)
-                self.wait_for[stage[i]] = max(self.wait_for[stage[i]], readers[i])
-        self.boundary = sorted(self.boundary)
-        self.streams = [engine.stream] + [torch.cuda.Stream(device=self.device) for _ in range(K - 1)]
+        self.cu_share = cu_share
+        if cu_share:
+            self.streams = [cu_masked_stream(self.device, _cu_mask(k, cu_share)) for k in range(K)]
+            engine.stream = self.streams[0]
+        else:
+            self.streams = [engine.stream] + [torch.cuda.Stream(device=self.device) for _ in range(K - 1)]
         self.stream = self.streams[0]
         self.done = [[torch.cuda.Event() for _ in range(K)] for _ in range(2)]   # [parity][stage]
         self._fork = torch.cuda.Event()

@@ -52,6 +52,7 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            128: (6, 6, 1, 4), 129: (6, 6, 1, 4), 130: (6, 6, 1, 4),
            131: (6, 6, 1, 4), 132: (6, 6, 1, 4), 133: (6, 6, 1, 4), 134: (6, 6, 1, 4),
            135: (12, 3, 1, 4), 136: (8, 3, 1, 4), 137: (12, 3, 1, 4), 138: (6, 6, 1, 4), 139: (4, 6, 1, 4),
+           140: (4, 3, 1, 4), 141: (4, 3, 1, 4), 142: (2, 6, 1, 4),
            # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
            160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
            165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
@@ -70,7 +71,7 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 104: 12,
            **{i: 12 for i in range(112, 118)},
            120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9, 128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 134: 9,
-           135: 15, 136: 11, 137: 15, 138: 9, 139: 8}
+           135: 15, 136: 11, 137: 15, 138: 9, 139: 8, 140: 8, 141: 8, 142: 8}
 ABLATION_IDS = frozenset(list(range(43, 61)) + list(range(112, 118)) + list(range(127, 135)) + [138, 139])   # 127+: s_memtime stamping
 # staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
 SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}

@@ -11,6 +11,7 @@ Routes (TF-Serving REST semantics):
 from __future__ import annotations
 
 import json
+import time
 import re
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -81,6 +82,7 @@ def make_handler(manager: ModelManager):
             m = _ROUTE.match(self.path)
             if not m or m.group("tail") != ":predict":
                 return self._send(404, {"error": "not found"})
+            t0 = time.perf_counter()
             try:
                 n = int(self.headers.get("Content-Length", "0"))
                 body = json.loads(self.rfile.read(n) or b"{}")
@@ -107,9 +109,17 @@ def make_handler(manager: ModelManager):
                 x = np.ascontiguousarray(x)
                 dl = self.headers.get("X-Deadline-Ms")
                 deadline = int(_lib.rt().now_us() + float(dl) * 1e3) if dl else 0
+                t1 = time.perf_counter()
                 out = runner.predict(x, x.shape[0], deadline).tolist()
+                t2 = time.perf_counter()
+                r = self._send(200, {"predictions": out} if rows else {"outputs": out})
+                # same per-request stage trace as the gRPC path (SURVEY.md §5 tracing)
+                METRICS.observe("kdl_stage_ms", (t1 - t0) * 1e3, stage="parse")
+                METRICS.observe("kdl_stage_ms", (t2 - t1) * 1e3, stage="batch_and_run")
+                METRICS.observe("kdl_stage_ms", (time.perf_counter() - t2) * 1e3, stage="respond")
                 METRICS.inc("kdl_requests_total", code="OK", method="RestPredict")
-                return self._send(200, {"predictions": out} if rows else {"outputs": out})
+                METRICS.observe("kdl_request_latency_ms", (time.perf_counter() - t0) * 1e3, method="RestPredict")
+                return r
             except ServingError as e:
                 METRICS.inc("kdl_requests_total", code=e.code, method="RestPredict")
                 return self._err(e)
