@@ -362,6 +362,9 @@ PYBIND11_MODULE(_C, m) {
         op.mem_bytes = bytes; p.add(op);
       })
       .def("set_cfg", [](Program& p, size_t i, int cfg) { p.mutable_op(i).cfg = cfg; })
+      .def("set_branch", [](Program& p, size_t i, int branch, int join) {
+        p.mutable_op(i).branch = branch; p.mutable_op(i).join = join;
+      })
       .def("cfg", [](const Program& p, size_t i) { return p.op(i).cfg; })
       .def("op_names", [](const Program& p) {
         std::vector<std::string> v;

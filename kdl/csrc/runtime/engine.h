@@ -42,6 +42,11 @@ struct Op {
   GemmF8Args f8{};
   void* mem_ptr = nullptr;
   size_t mem_bytes = 0;
+  // graph-level concurrency (capture only; eager runs stay sequential): branch = 1 ops
+  // run on a side stream forked from the main one at the first such op; join = 1 makes
+  // this (main-stream) op wait for the side branch (Xception: the residual 1x1 conv of
+  // an entry/exit block runs beside the block's separable convs, joined at the pool)
+  int branch = 0, join = 0;
 };
 
 void check_hip(hipError_t e, const std::string& what);

@@ -95,7 +95,7 @@ class EngineBase:
         self._slot = slot
         try:
             for step in self.steps:
-                self._emit(prog, step, b)
+                self._emit_marked(prog, step, b)
         finally:
             self._slot = 0
         if capture:
@@ -130,7 +130,7 @@ class EngineBase:
         try:
             for step, m in zip(self.steps[lo:hi], maps):
                 self._remap = m
-                self._emit(prog, step, b)
+                self._emit_marked(prog, step, b)
         finally:
             self._slot, self._remap = 0, {}
         if capture:
@@ -138,6 +138,17 @@ class EngineBase:
                 prog.capture(int(self.stream.cuda_stream))
         self.programs[key] = prog
         return prog
+
+    def _emit_marked(self, prog, step: Step, b: int) -> None:
+        """Emit one step and carry its graph-concurrency marks onto its ops: extra
+        ``branch`` = the step's ops run on the captured graph's side branch, ``join`` =
+        the step waits for that branch first (native Program.capture)."""
+        n0 = len(prog)
+        self._emit(prog, step, b)
+        br, jn = int(step.extra.get("branch", 0)), int(step.extra.get("join", 0))
+        if br or jn:
+            for i in range(n0, len(prog)):
+                prog.set_branch(i, br, jn if i == n0 else 0)
 
     def invalidate(self) -> None:
         self.programs.clear()

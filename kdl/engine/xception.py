@@ -17,6 +17,7 @@ The reference equivalent is TF-Serving's SavedModel session run
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 
 import torch
@@ -39,6 +40,11 @@ class XceptionEngine(EngineBase):
         super().__init__(device, max_batch, buckets)
         self.in_kind = in_kind
         self.head = head
+        # KDL_BRANCHES=1: residual convs on a side branch of the captured graph. Off by
+        # default: a forked hipGraph measured 16 % SLOWER in the stage-pipelined bench
+        # (17.7k vs 21.1k img/s, profiles/stages_ab.txt) -- the graph's second branch
+        # competes for the hardware queues the two stages already use
+        self.branches = int(os.environ.get("KDL_BRANCHES", "0"))
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
@@ -80,7 +86,10 @@ class XceptionEngine(EngineBase):
                 oh = (H - 1) // 2 + 1
                 rname = f"{rc.name}_out"
                 lay = self._pw(p, rc, dev)
-                self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh)))
+                # the residual 1x1/2 conv only depends on the block input: in the captured
+                # graph it runs on a side branch beside the block's separable convs
+                self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh),
+                                       extra=dict(branch=self.branches)))
                 self.shapes[rname] = (oh, oh, lay.ldy)
                 y = cur
                 for op in blk.main:
@@ -93,7 +102,7 @@ class XceptionEngine(EngineBase):
                 out = f"block{bi + 1}_out"
                 C = self.shapes[y][2]
                 self.steps.append(Step("pool", f"block{bi + 1}_pool", src=y, dst=out, res=rname,
-                                       geom=(H, H, oh, oh), extra=dict(pad=pt, C=C)))
+                                       geom=(H, H, oh, oh), extra=dict(pad=pt, C=C, join=self.branches)))
                 self.shapes[out] = (oh, oh, C)
                 cur, H = out, oh
             elif blk.kind == "middle":
