@@ -228,21 +228,38 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
 // applies bias + SiLU, then its 256 channels run fc2 with the TRANSPOSED w2 ([Cs][C]:
 // coalesced across threads, independent loads) and the sigmoid.
 // One workgroup per image. The tile partials of the fused pool (ntiles x Cs floats) are
-// summed by all 256 threads with coalesced loads into LDS (ds_add_f32): the previous
-// form looped over the tiles serially in Cs threads and recomputed that sum in every
-// channel block of the grid, ~35 us per call on B7 (8 % of the forward) for a few
-// hundred thousand MACs (profiles/efficientnet_b7_b32_bench_layers.txt).
+// summed by all 256 threads: G = 256 / Cs thread groups each sum every G-th tile of
+// every unit in a fixed order, then one thread per unit adds the G group sums in order
+// (deterministic: atomics would make the sums order-dependent, and 55 blocks of SiLU
+// amplify that run-to-run). The previous form looped over the tiles serially in Cs
+// threads and recomputed that sum in every channel block of the grid, ~35 us per call
+// on B7 (8 % of the forward) for a few hundred thousand MACs.
 __global__ __launch_bounds__(256) void se_kernel(SeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float hid[];   // [Cs]
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // [256] group sums, [Cs] hidden
+  float* part = sm;
+  float* hid = sm + 256;
   const int b = blockIdx.x, tid = threadIdx.x;
-  for (int j = tid; j < a.Cs; j += 256) hid[j] = 0.f;
-  __syncthreads();
   const float* pb = a.pool + (long)b * a.ntiles * a.Cs;
-  const int n = a.ntiles * a.Cs;
-  for (int i = tid; i < n; i += 256) atomicAdd(&hid[i % a.Cs], pb[i]);
+  const int G = a.Cs <= 256 ? 256 / a.Cs : 1;
+  if (a.Cs <= 256) {
+    const int g = tid / a.Cs, j = tid - g * a.Cs;
+    if (g < G) {
+      float h = 0.f;
+      for (int t = g; t < a.ntiles; t += G) h += pb[(long)t * a.Cs + j];
+      part[g * a.Cs + j] = h;
+    }
+  }
   __syncthreads();
   const float inv = 1.f / (float)a.HW;
-  for (int j = tid; j < a.Cs; j += 256) hid[j] = silu(hid[j] * inv + a.b1[j]);
+  for (int j = tid; j < a.Cs; j += 256) {
+    float h = 0.f;
+    if (a.Cs <= 256) {
+      for (int g = 0; g < G; ++g) h += part[g * a.Cs + j];
+    } else {
+      for (int t = 0; t < a.ntiles; ++t) h += pb[(long)t * a.Cs + j];
+    }
+    hid[j] = silu(h * inv + a.b1[j]);
+  }
   __syncthreads();
   for (int c = tid; c < a.C; c += 256) {
     float s = a.b2[c];
@@ -254,7 +271,7 @@ __global__ __launch_bounds__(256) void se_kernel(SeArgs a) {
 
 hipError_t squeeze_excite(const SeArgs& a, hipStream_t s) {
   if (a.B <= 0 || a.Cs <= 0 || a.ntiles <= 0) return hipErrorInvalidValue;
-  const size_t smem = (size_t)a.Cs * sizeof(float);
+  const size_t smem = (size_t)(256 + a.Cs) * sizeof(float);
   hipLaunchKernelGGL(se_kernel, dim3(a.B), dim3(256), smem, s, a);
   return hipGetLastError();
 }
