@@ -5,21 +5,24 @@ and p50 batch latency on 1..8 MI355X (BASELINE.json metric/config).
 One process per GPU (``torch.distributed.run``), RCCL over xGMI. A timed step is
 one dynamic batch of 32 images per GPU (weak scaling, global batch 32*N):
 
-  1. ingress: rank 0 copies the uint8 batch [32N,299,299,3] host(pinned)->device
-     on a copy stream;
-  2. scatter: RCCL scatter of uint8 shards (4x fewer bytes than f32)
-     on a comm stream, straight into one of every rank's two engine input slots;
-  3. forward: hipGraph replays of the fused HIP-kernel model: the batch runs as
-     two concurrent 16-image lanes on two streams (``--lanes``,
-     kdl/engine/lanes.py), one lane's layer tails overlapping the other's body;
-  4. gather:  RCCL gather of the fp32 logits to rank 0 + D2H, both on the comm
-     stream (one GPU: D2H on an egress stream), so compute / lane / H2D / comm
-     streams each own one of the 4 hardware queues.
-Steps are software-pipelined: batch i+1's H2D + scatter overlap batch i's forward.
+  1. ingress (default ``--ingress local``): every rank copies its own uint8 batch
+     [32,299,299,3] host(pinned)->device on a copy stream, straight into one of its
+     engine's input slots -- what the server's per-GPU executors do with their pinned
+     staging (kdl/serving/backend.py). Each GPU has its own PCIe link;
+  2. forward: hipGraph replays of the fused HIP-kernel model, stage-pipelined
+     (kdl/engine/stages.py: stage 1 of batch i+1 runs beside stage 2 of batch i);
+  3. gather: RCCL gather of the fp32 logits to rank 0 + D2H on a comm stream (one
+     GPU: D2H behind the last stage), so compute stages / H2D / comm each own one
+     of the 4 hardware queues.
+Steps are software-pipelined: batch i+depth's H2D overlaps batch i's forward.
 
-``--ingress local`` instead has every rank H2D its own shard (host-direct mode,
-no rank-0 bottleneck). Data is synthetic (random uint8 images) and the weights are
-random-init of the exact architecture (no network for checkpoints).
+``--ingress scatter`` is the single-ingress variant: rank 0 H2Ds the
+whole node's batch [32N,...] and RCCL-scatters uint8 shards (4x fewer bytes than f32)
+over xGMI. Measured pinned H2D on one MI355X: 50 GB/s, so rank 0's 68.7 MB per step at
+N=8 takes 1.37 ms against a 1.5 ms forward (profiles/h2d_bandwidth.txt): the rank-0
+PCIe link, not xGMI, would bound the node, which is why it is not the default. Data
+is synthetic (random uint8 images) and the weights are random-init of the exact
+architecture (no network for checkpoints).
 """
 from __future__ import annotations
 
@@ -47,8 +50,8 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--model", default="xception",
                     help="xception (headline) | resnet50 | vit_b16 | vit_b16_fp8 | efficientnet_b7")
-    ap.add_argument("--ingress", choices=["scatter", "local", "none"], default="scatter",
-                    help="none: DIAGNOSTIC ONLY (no host->device copy; the graphs re-read stale "
+    ap.add_argument("--ingress", choices=["scatter", "local", "none"], default="local",
+                    help="local: each rank H2Ds its own batch; scatter: rank 0 H2Ds all and RCCL-scatters; none: DIAGNOSTIC ONLY (no host->device copy; the graphs re-read stale "
                          "slots) to measure what ingress overlap costs; never a reported number")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--depth", type=int, default=3,
@@ -128,7 +131,7 @@ def main(argv=None) -> int:
 
     g = torch.Generator().manual_seed(1234 + rank)
     n_global = B * world
-    # synthetic request batch in pinned host memory (rank 0 = ingress for scatter).
+    # synthetic request batch in pinned host memory (every rank; only rank 0 for scatter).
     # Ingress is double-buffered: the H2D of batch i+1 runs on a copy stream while
     # batch i computes (what the serving executor does with its pinned staging).
     n_host = n_global if a.ingress == "scatter" else B
