@@ -283,6 +283,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   static_assert(BM == TH * TW && TW % 16 == 0, "the M tile is TH x TW pixels, 16-pixel row segments");
   static_assert(NW % 2 == 0 && STAGES >= 3, "loader/storer halves; >= 1 patch in flight across barriers");
+  static_assert(BN <= 256, "the bias is one 1 KiB DMA");
   using P = S2dPatch<TH, TW>;
   constexpr int AF = BM / 16, BF = BN / 16;
   constexpr int IPP = P::IPP, XB = P::XB;
@@ -307,12 +308,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
   const int TWn = t0 < ntiles ? (ntiles - t0 + G - 1) / G : 0;   // tiles of this workgroup
   const int Q = TWn * KT;                                         // stages
   if (Q == 0) return;                           // uniform per workgroup; nothing issued yet
-  // LDS map: [B resident KT*BF KiB][dw entries KT KiB][ring][A x2][C tile]
+  // LDS map: [B resident KT*BF KiB][dw entries KT KiB][ring][A x2][C tile][bias 1 KiB]
   uint8_t* const bres = smem;
   uint8_t* const dres = smem + KT * BF * 1024;
   uint8_t* const ring = dres + KT * 1024;
   uint8_t* const abuf = ring + STAGES * STAGE;
   uint8_t* const ctile = abuf + 2 * ABUF;
+  uint8_t* const bias = ctile + BM * CS;
 
   // ---- resident weights (all waves), then the ring prologue (loader waves)
   for (int idx = wave; idx < KT * BF; idx += NW) {
@@ -320,6 +322,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
     glds16(a.wp + ((long)f * KT + k) * 512 + lane * 8, bres + idx * 1024);
   }
   for (int k = wave; k < KT; k += NW) glds16((const uint8_t*)a.dwk + k * 1024 + lane * 16, dres + k * 1024);
+  // the bias rides the same DMA path into LDS: a global load of it in the tile epilogue made
+  // the compiler put a vmcnt(0) there, which drained the loader waves' whole ring (every
+  // in-flight patch) at every tile boundary
+  if (wave == NW - 1) glds16((const uint8_t*)(a.bias + min(lane * 4, BN - 4)), bias + lane * 16);
 
   // loader lanes: patch slot geometry of each of this wave's LX instructions
   int pq[LX], prr[LX], pcc[LX], pis[LX];
@@ -332,24 +338,40 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
     pcc[i] = slot - prr[i] * P::PW;
     pis[i] = slot < P::PS;
   }
-  auto issue = [&](int qs, int slotbuf) {     // stage qs (wave-uniform) into ring slot slotbuf
-    const int ti = qs / KT, k = qs - ti * KT;
+  // issue cursor: stages go out in (tile, k) order, one per call; past the last stage the
+  // cursor stays put and re-issues it (keeps every wave's DMA count per stage fixed). The
+  // patch sources of a tile are computed once, when the cursor enters it (the divisions
+  // per call cost ~70 scalar instructions per k-step).
+  int iq = 0, ik = 0, iti = 0;
+  const uint8_t* psrc[LX];
+  auto enter_tile = [&](int ti) {
     const int tile = t0 + ti * G;
     const int bimg = tile / (nth * ntw), trem = tile - bimg * (nth * ntw);
     const int h0 = (trem / ntw) * TH, w0 = (trem % ntw) * TW;
-    uint8_t* base = ring + slotbuf * STAGE;
 #pragma unroll
     for (int i = 0; i < LX; ++i) {
-      const int sidx = min(wave + i * NL, XB - 1);
       const int h = h0 - 1 + prr[i], w = w0 - 1 + pcc[i];
       const bool in = pis[i] && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-      const uint8_t* src = in ? (const uint8_t*)(a.x + (((long)bimg * H + h) * W + w) * a.ldx + pq[i] * 8) : s2d_zeros;
-      glds16(src + k * 64, base + sidx * 1024);
+      psrc[i] = in ? (const uint8_t*)(a.x + (((long)bimg * H + h) * W + w) * a.ldx + pq[i] * 8) : s2d_zeros;
+    }
+  };
+  auto issue = [&](int slotbuf) {             // the cursor's stage into ring slot slotbuf
+    uint8_t* base = ring + slotbuf * STAGE;
+#pragma unroll
+    for (int i = 0; i < LX; ++i) glds16(psrc[i] + ik * 64, base + min(wave + i * NL, XB - 1) * 1024);
+    if (iq + 1 < Q) {
+      ++iq;
+      if (++ik == KT) {
+        ik = 0;
+        enter_tile(++iti);
+      }
     }
   };
   const bool loader = wave < NL;
-  if (loader)
-    for (int p = 0; p < STAGES - 1; ++p) issue(min(p, Q - 1), p);
+  if (loader) {
+    enter_tile(0);
+    for (int p = 0; p < STAGES - 1; ++p) issue(p);
+  }
 
   // ---- depthwise units (as in sepconv_2d_kernel)
   const int g = wave & 1;
@@ -440,13 +462,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
   }
 
   const int quad = lane >> 4, col = lane & 15;
+  // bias of this wave's output columns, read once (an LDS read in the tile epilogue got a
+  // conservative vmcnt(0) from the compiler: pending LDS-DMAs may alias it)
+  float4 bvr[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bvr[j] = *(const float4*)(bias + (wn * FN * 16 + j * 16 + 4 * quad) * 4);
   int k = 0, ti = 0;
   for (int q = 0; q < Q; ++q) {
     // stage q+1 landed; STAGES-3 younger patches stay in flight (loaders' counters hold
     // only DMAs); storers hold only stores and may retire them lazily
     if (loader) s2_wait_barrier<(STAGES - 3) * LX>();
     else s2_wait_barrier<63>();
-    if (loader) issue(min(q + STAGES - 1, Q - 1), (q + STAGES - 1) % STAGES);
+    if (loader) issue((q + STAGES - 1) % STAGES);
     const uint8_t* As = abuf + (q & 1) * ABUF + lane * 16;
     const uint8_t* Bs = bres + k * BF * 1024 + lane * 16;
     s16x8 af[FM], bf[FN];
@@ -472,7 +499,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int nl = wn * FN * 16 + j * 16 + 4 * quad;
-        const float4 bv = *(const float4*)(a.bias + nl);
+        const float4 bv = bvr[j];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int mll = wm * FM * 16 + i * 16 + col;
@@ -511,7 +538,10 @@ constexpr int S2DP_OFFSET = 24;
   X(2, 2, 4, 2, 4, 3, 4, 16)    \
   X(3, 4, 2, 2, 4, 4, 8, 16)    \
   X(4, 3, 2, 2, 4, 6, 6, 16)    \
-  X(5, 2, 4, 2, 4, 4, 4, 16)
+  X(5, 2, 4, 2, 4, 4, 4, 16)    \
+  X(6, 2, 2, 2, 4, 8, 4, 16)    \
+  X(7, 2, 2, 2, 4, 11, 4, 16)   \
+  X(8, 3, 2, 2, 4, 7, 6, 16)
 
 template <int FM, int FN, int WGM, int WGN, int STAGES, int TH, int TW>
 static size_t s2dp_smem(int K) {
@@ -519,7 +549,7 @@ static size_t s2dp_smem(int K) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   const int KT = K / 32;
   return (size_t)KT * (BN / 16) * 1024 + (size_t)KT * 1024 + (size_t)STAGES * P::XB * 1024 + 2 * (BM / 16) * 1024 +
-         (size_t)BM * (BN * 2 + 16);
+         (size_t)BM * (BN * 2 + 16) + 1024;
 }
 
 static int s2dp_num_cus() {

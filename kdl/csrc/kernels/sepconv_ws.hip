@@ -80,6 +80,15 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   // band: raster pixels P0 .. P0+NS-1 = every 3x3 neighbour of the tile's pixels, as 4
   // planes (one per 8-channel chunk) of NSP 16-byte slots; slot NSP-1 stays zero
   const long P0 = (long)m0 - W - 1;
+  // ABL bit 32: every M tile walks K from its own starting chunk (the two N tiles of an M
+  // tile share it, so their band reads stay L2-shared): without it all workgroups fetch the
+  // same weight fragments at the same time
+  int krot = 0;
+  if constexpr ((ABL & 32) != 0) krot = (mi * 7) % KT;
+  auto kc = [&](int t) {
+    t = min(t, KT - 1) + krot;
+    return t >= KT ? t - KT : t;
+  };
   const int NS = min(m0 + BM, a.M) - m0 + 2 * W + 2;
 
   f32x4 acc[FM][FN];
@@ -121,7 +130,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
     // stages past the end (the branch-free loop keeps issuing) re-load the last one (a scalar
     // clamp; a per-lane select to a zero block cost more VALU than the drain it saves)
     auto issue_band = [&](int t, int slot) {
-      t = min(t, KT - 1);
+      t = kc(t);
 #pragma unroll
       for (int i = 0; i < LCB; ++i) glds16(xsrc[i] + t * 64, smem + slot * STAGE + min(wn + 4 * i, XB - 1) * 1024);
     };
@@ -132,7 +141,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
     };
     auto load_b = [&](int t, s16x8 (&b)[FN]) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) gload(b[j], bsrc + j * bstride + (long)min(t, KT - 1) * 1024);
+      for (int j = 0; j < FN; ++j) gload(b[j], bsrc + j * bstride + (long)kc(t) * 1024);
     };
     auto step = [&](int t, s16x8 (&b)[FN]) {
       ws_wait_barrier<WC>();
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
 #pragma unroll
           for (int i = 0; i < FM; ++i) acc[i][j] = mfma16(b[j], af[i], acc[i][j]);
         }
-        gload(b[j], bsrc + j * bstride + (long)min(t + 2, KT - 1) * 1024);
+        gload(b[j], bsrc + j * bstride + (long)kc(t + 2) * 1024);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, FM, 0);      // A fragment reads
 #pragma unroll
@@ -189,7 +198,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
     // ================= producer: dw weights LDS-DMA, depthwise on MFMA
     const int pw = wave - 4;
     const uint8_t* wsrc = (const uint8_t*)a.dwk + lane * 16;
-    auto issue = [&](int t, int slot) { glds16(wsrc + (long)min(t, KT - 1) * 1024, smem + slot * STAGE + WOFF); };
+    auto issue = [&](int t, int slot) { glds16(wsrc + (long)kc(t) * 1024, smem + slot * STAGE + WOFF); };
 
     const int g = pw & 1;                        // channel group of all this wave's units
     const int p16 = lane & 15, kb = lane >> 4;
@@ -358,15 +367,20 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(19, 4, 6, 5, 8)          \
   X(20, 4, 3, 5, 8)          \
   X(21, 4, 3, 6, 8)          \
-  X(22, 2, 6, 5, 8)
+  X(22, 2, 6, 5, 8)          \
+  X(23, 6, 6, 5, 9)          \
+  X(24, 6, 6, 5, 11)         \
+  X(25, 6, 6, 5, 16)         \
+  X(26, 4, 6, 5, 8)
 
 // timing-ablation bits of the stamping ids: 1 no depthwise MFMA, 2 no pointwise MFMA,
 // 4 no band / weight LDS-DMA in the loop, 8 producers skip the depthwise entirely;
 // ids 18/19 (no stamps): 16 = band DMA'd as 16 pixels x 64 B per instruction (wrong LDS
-// placement for the producers: timing only)
+// placement for the producers: timing only); ids 23-26 = 0, 2, 3, 5 with bit 32 (per-M-tile
+// rotated K order)
 constexpr int sepw_abl(int id) {
   return id == 8 ? 1 : id == 9 ? 2 : id == 10 ? 3 : id == 11 ? 4 : id == 12 ? 5 : id == 13 ? 8 : id == 14 ? 12
-       : id == 18 || id == 19 ? 16 : 0;
+       : id == 18 || id == 19 ? 16 : id >= 23 && id <= 26 ? 32 : 0;
 }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }

@@ -53,15 +53,18 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            131: (6, 6, 1, 4), 132: (6, 6, 1, 4), 133: (6, 6, 1, 4), 134: (6, 6, 1, 4),
            135: (12, 3, 1, 4), 136: (8, 3, 1, 4), 137: (12, 3, 1, 4), 138: (6, 6, 1, 4), 139: (4, 6, 1, 4),
            140: (4, 3, 1, 4), 141: (4, 3, 1, 4), 142: (2, 6, 1, 4),
+           # 143-146 = 120, 122, 123, 125 walking K from a per-M-tile rotated start (ABL bit 32)
+           143: (6, 6, 1, 4), 144: (6, 6, 1, 4), 145: (6, 6, 1, 4), 146: (4, 6, 1, 4),
            # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
            160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
            165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
            170: (3, 2, 2, 4), 171: (2, 2, 2, 4), 172: (2, 2, 2, 4), 173: (3, 4, 2, 4),
            # persistent 2-D tiled variant (sepconv_2dp_kernel, KDL_S2DP_CONFIGS): weights LDS-resident
            184: (3, 2, 2, 4), 185: (2, 2, 2, 4), 186: (2, 4, 2, 4), 187: (4, 2, 2, 4), 188: (3, 2, 2, 4),
-           189: (2, 4, 2, 4)}
+           189: (2, 4, 2, 4), 190: (2, 2, 2, 4), 191: (2, 2, 2, 4), 192: (3, 2, 2, 4)}
 # persistent 2-D variant: (STAGES, TH, TW) per id, mirror of KDL_S2DP_CONFIGS (LDS sizing)
-S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188: (6, 6, 16), 189: (4, 4, 16)}
+S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188: (6, 6, 16), 189: (4, 4, 16),
+        190: (8, 4, 16), 191: (11, 4, 16), 192: (7, 6, 16)}
 SEP_BASE = 64
 SEPP_BASE = 96
 SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
@@ -71,7 +74,8 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 104: 12,
            **{i: 12 for i in range(112, 118)},
            120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9, 128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 134: 9,
-           135: 15, 136: 11, 137: 15, 138: 9, 139: 8, 140: 8, 141: 8, 142: 8}
+           135: 15, 136: 11, 137: 15, 138: 9, 139: 8, 140: 8, 141: 8, 142: 8,
+           143: 9, 144: 11, 145: 16, 146: 8}
 ABLATION_IDS = frozenset(list(range(43, 61)) + list(range(112, 118)) + list(range(127, 135)) + [138, 139])   # 127+: s_memtime stamping
 # staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
 SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
@@ -83,7 +87,7 @@ def s2dp_smem(cfg: int, K: int) -> int:
     bm, bn = cfg_tile(cfg)
     ipp = ((th + 2) * (tw + 2) + 1 + 63) // 64
     kt = K // 32
-    return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024 + bm * (bn * 2 + 16)
+    return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024 + bm * (bn * 2 + 16) + 1024
 
 
 def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | None = None) -> bool:
