@@ -41,6 +41,8 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.nstore = I(d, "nstore"); a.stride = I(d, "stride", 1);
   a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out"); a.opad = I(d, "opad");
   a.dt = I(d, "dt");
+  a.px = P<const uint16_t>(d, "px");
+  a.pH = I(d, "pH"); a.pW = I(d, "pW"); a.pld = I(d, "pld"); a.ppad = I(d, "ppad");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {

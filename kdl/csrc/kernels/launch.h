@@ -33,6 +33,12 @@ struct ConvGemmArgs {
                          //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
                          // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
   int dt;                // element type of x / wp / res / y: 0 bf16, 1 fp16 (MODE_PW / MODE_CONV GEMMs)
+  // optional fused TF-'same' 3x3/2 max-pool (Xception entry/exit blocks): the epilogue adds
+  // maxpool(px)[m] to the GEMM output, px = [B][pH][pW][pld] bf16, leading pad ppad. The
+  // residual 1x1/2 conv then writes the block output directly: no pool kernel, and the
+  // conv result never round-trips through HBM (epilogue.h)
+  const uint16_t* px;
+  int pH, pW, pld, ppad;
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);

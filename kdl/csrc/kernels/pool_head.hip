@@ -6,25 +6,26 @@
 
 namespace kdl {
 
-// One thread = one output pixel x 8 channels. TF 'same' pads with -inf, i.e.
-// out-of-range taps are skipped (the odd pad goes bottom/right: pad_top/left
-// are the *leading* pads computed on the host).
+// One thread = one output pixel x 8 channels; grid (ceil(OW*C/8 / 256), B*OH): the output
+// row comes from blockIdx.y (scalar), so the only per-thread index math is one 32-bit
+// division by C/8. (The flat-index version spent ~200 VALU instructions per thread on
+// four 64-bit div/mods -- as much VALU time as the 267 MB it moves at b32 / 147x147.)
+// TF 'same' pads with -inf, i.e. out-of-range taps are skipped (the odd pad goes
+// bottom/right: pad_top/left are the *leading* pads computed on the host).
 template <int DT>
 __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
   using E = Elt<DT>;
   const int CC = a.C >> 3;
-  const long total = (long)a.B * a.OH * a.OW * CC;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int cc = (int)(i % CC);
-  const long p = i / CC;  // output pixel
-  const int ow = (int)(p % a.OW);
-  const long t = p / a.OW;
-  const int oh = (int)(t % a.OH);
-  const int b = (int)(t / a.OH);
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.OW * CC) return;
+  const int row = blockIdx.y;                   // b * OH + oh
+  const int b = row / a.OH, oh = row - b * a.OH;
+  const int ow = (unsigned)j / (unsigned)CC, cc = j - ow * CC;
+  const long p = (long)row * a.OW + ow;         // output pixel
   float mx[8];
 #pragma unroll
   for (int d = 0; d < 8; ++d) mx[d] = -INFINITY;
+  const uint16_t* xb = a.x + (long)b * a.H * a.W * a.C + cc * 8;
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
     const int ih = oh * 2 - a.pad_top + dy;
@@ -33,7 +34,7 @@ __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
     for (int dx = 0; dx < 3; ++dx) {
       const int iw = ow * 2 - a.pad_left + dx;
       if ((unsigned)iw >= (unsigned)a.W) continue;
-      const u32x4 v = *(const u32x4*)(a.x + (((long)b * a.H + ih) * a.W + iw) * a.C + cc * 8);
+      const u32x4 v = *(const u32x4*)(xb + (long)(ih * a.W + iw) * a.C);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         mx[2 * d] = fmaxf(mx[2 * d], E::lo(v[d]));
@@ -56,10 +57,11 @@ __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
 }
 
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
-  if (a.C % 8 != 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
-  const long total = (long)a.B * a.OH * a.OW * (a.C / 8);
-  if (a.dt) hipLaunchKernelGGL(pool_add_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(pool_add_kernel<0>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  if (a.C % 8 != 0 || a.dt < 0 || a.dt > 1 || a.B <= 0 || a.OH <= 0 || a.OW <= 0) return hipErrorInvalidValue;
+  if ((long)a.B * a.OH > 65535) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((a.OW * (a.C / 8) + 255) / 256), (unsigned)(a.B * a.OH));
+  if (a.dt) hipLaunchKernelGGL(pool_add_kernel<1>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(pool_add_kernel<0>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
 #pragma unroll
           for (int i = 0; i < FM; ++i) acc[i][j] = mfma16(b[j], af[i], acc[i][j]);
         }
-        gload(b[j], bsrc + j * bstride + (long)kc(t + 2) * 1024);
+        if constexpr (!(ABL & 64)) gload(b[j], bsrc + j * bstride + (long)kc(t + 2) * 1024);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, FM, 0);      // A fragment reads
 #pragma unroll
@@ -371,16 +371,18 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(23, 6, 6, 5, 9)          \
   X(24, 6, 6, 5, 11)         \
   X(25, 6, 6, 5, 16)         \
-  X(26, 4, 6, 5, 8)
+  X(26, 4, 6, 5, 8)          \
+  X(27, 6, 6, 6, 9)
 
 // timing-ablation bits of the stamping ids: 1 no depthwise MFMA, 2 no pointwise MFMA,
 // 4 no band / weight LDS-DMA in the loop, 8 producers skip the depthwise entirely;
 // ids 18/19 (no stamps): 16 = band DMA'd as 16 pixels x 64 B per instruction (wrong LDS
 // placement for the producers: timing only); ids 23-26 = 0, 2, 3, 5 with bit 32 (per-M-tile
-// rotated K order)
+// rotated K order); id 27 = stamping with bit 64 (consumers never reload their pointwise
+// weight registers: timing only)
 constexpr int sepw_abl(int id) {
   return id == 8 ? 1 : id == 9 ? 2 : id == 10 ? 3 : id == 11 ? 4 : id == 12 ? 5 : id == 13 ? 8 : id == 14 ? 12
-       : id == 18 || id == 19 ? 16 : id >= 23 && id <= 26 ? 32 : 0;
+       : id == 18 || id == 19 ? 16 : id >= 23 && id <= 26 ? 32 : id == 27 ? 64 : 0;
 }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }
@@ -418,10 +420,10 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 #define KDL_SWCASE(id, fm, fn, st, xb)                                                                \
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, (id >= 7 && id <= 14), sepw_abl(id), true>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, ((id >= 7 && id <= 14) || id == 27), sepw_abl(id), true>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     else                                                                                            \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, (id >= 7 && id <= 14), sepw_abl(id), false>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, ((id >= 7 && id <= 14) || id == 27), sepw_abl(id), false>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)

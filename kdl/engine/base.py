@@ -84,7 +84,7 @@ class EngineBase:
     # ---------------------------------------------------------------- programs
     def conv_steps(self) -> list[Step]:
         """Steps with a tunable GEMM layer (bf16 conv-GEMM or fp8 linear)."""
-        return [s for s in self.steps if s.kind in ("conv", "f8")]
+        return [s for s in self.steps if s.kind in ("conv", "convpool", "f8")]
 
     def program(self, b: int, capture: bool = True, slot: int = 0):
         key = (b, capture, slot)

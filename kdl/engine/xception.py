@@ -5,7 +5,8 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
     stem_conv            block1_conv1 + BN + ReLU (normalisation folded, uint8 in)
     conv_gemm MODE_CONV  block1_conv2 3x3 + BN + ReLU (implicit GEMM)
     conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
-    conv_gemm MODE_PW    residual 1x1/2 convs + BN
+    conv_gemm MODE_PW    residual 1x1/2 convs + BN (KDL_POOLFUSE=1: with the block's
+                         3x3/2 max-pool of the main branch added in the epilogue, "convpool")
     pool_add             TF-'same' 3x3/2 max-pool + residual add
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
 
@@ -45,6 +46,12 @@ class XceptionEngine(EngineBase):
         # (17.7k vs 21.1k img/s, profiles/stages_ab.txt) -- the graph's second branch
         # competes for the hardware queues the two stages already use
         self.branches = int(os.environ.get("KDL_BRANCHES", "0"))
+        # KDL_POOLFUSE=1: residual 1x1/2 conv + block max-pool as ONE launch (the pool in the
+        # conv's epilogue, step kind "convpool"). Off by default: measured 3 % SLOWER in the
+        # stage-pipelined bench (20.8-20.9k vs 21.5k img/s, same box): the epilogue's nine
+        # dependent 16-B pool reads per output chunk are latency-bound inside the GEMM's store
+        # loop, so the fused launch (80.8 us at block2) costs what conv + pool_add did (82.6)
+        self.poolfuse = os.environ.get("KDL_POOLFUSE", "0") == "1" and not self.branches
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
@@ -86,11 +93,13 @@ class XceptionEngine(EngineBase):
                 oh = (H - 1) // 2 + 1
                 rname = f"{rc.name}_out"
                 lay = self._pw(p, rc, dev)
-                # the residual 1x1/2 conv only depends on the block input: in the captured
-                # graph it runs on a side branch beside the block's separable convs
-                self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh),
-                                       extra=dict(branch=self.branches)))
-                self.shapes[rname] = (oh, oh, lay.ldy)
+                rlay = lay
+                if not self.poolfuse:
+                    # the residual 1x1/2 conv only depends on the block input: in the captured
+                    # graph it may run on a side branch beside the block's separable convs
+                    self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh),
+                                           extra=dict(branch=self.branches)))
+                    self.shapes[rname] = (oh, oh, lay.ldy)
                 y = cur
                 for op in blk.main:
                     lay = self._sep(p, op, dev)
@@ -101,8 +110,15 @@ class XceptionEngine(EngineBase):
                 _, pt, _ = tf_same_pad(H, 3, 2)
                 out = f"block{bi + 1}_out"
                 C = self.shapes[y][2]
-                self.steps.append(Step("pool", f"block{bi + 1}_pool", src=y, dst=out, res=rname,
-                                       geom=(H, H, oh, oh), extra=dict(pad=pt, C=C, join=self.branches)))
+                if self.poolfuse:
+                    # residual conv of the block input, + maxpool(main branch) in its epilogue,
+                    # straight into the block output (reads: src = block input, res = main branch)
+                    assert rlay.ldy == C, (rc.name, rlay.ldy, C)
+                    self.steps.append(Step("convpool", rc.name, rlay, cur, out, res=y, geom=(H, H, oh, oh),
+                                           extra=dict(pad=pt)))
+                else:
+                    self.steps.append(Step("pool", f"block{bi + 1}_pool", src=y, dst=out, res=rname,
+                                           geom=(H, H, oh, oh), extra=dict(pad=pt, C=C, join=self.branches)))
                 self.shapes[out] = (oh, oh, C)
                 cur, H = out, oh
             elif blk.kind == "middle":
@@ -210,7 +226,7 @@ class XceptionEngine(EngineBase):
                                           bias=_lib.ptr(self.stem_bias), y=self._ptr(step.dst),
                                           B=b, H=H, W=W, OH=OH, OW=OW, ldy=32,
                                           in_kind=0 if self.in_kind == "u8" else 1))
-        elif step.kind == "conv":
+        elif step.kind in ("conv", "convpool"):
             self._emit_conv(prog, step, b)
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=self._ptr(step.res),
@@ -228,6 +244,12 @@ class XceptionEngine(EngineBase):
 
     def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
         H, W, OH, OW = step.geom
+        if step.kind == "convpool":
+            ph, pw, pc = self.shapes[step.res]
+            step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
+                            ldx=self.shapes[step.src][2], split=split, cfg=cfg,
+                            pool=dict(px=self._ptr(step.res), pH=ph, pW=pw, pld=pc, ppad=step.extra["pad"]))
+            return
         step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
                         res=self._ptr(step.res) if step.res else None, ldx=self.shapes[step.src][2],
                         ldr=self.shapes[step.res][2] if step.res else None, tmp=self._ptr("__dwtmp"),

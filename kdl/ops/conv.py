@@ -55,6 +55,7 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            140: (4, 3, 1, 4), 141: (4, 3, 1, 4), 142: (2, 6, 1, 4),
            # 143-146 = 120, 122, 123, 125 walking K from a per-M-tile rotated start (ABL bit 32)
            143: (6, 6, 1, 4), 144: (6, 6, 1, 4), 145: (6, 6, 1, 4), 146: (4, 6, 1, 4),
+           147: (6, 6, 1, 4),   # stamping + no B reloads (timing only)
            # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
            160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
            165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
@@ -75,8 +76,8 @@ SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 1
            **{i: 12 for i in range(112, 118)},
            120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9, 128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 134: 9,
            135: 15, 136: 11, 137: 15, 138: 9, 139: 8, 140: 8, 141: 8, 142: 8,
-           143: 9, 144: 11, 145: 16, 146: 8}
-ABLATION_IDS = frozenset(list(range(43, 61)) + list(range(112, 118)) + list(range(127, 135)) + [138, 139])   # 127+: s_memtime stamping
+           143: 9, 144: 11, 145: 16, 146: 8, 147: 9}
+ABLATION_IDS = frozenset(list(range(43, 61)) + list(range(112, 118)) + list(range(127, 135)) + [138, 139, 147])   # 127+: s_memtime stamping
 # staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
 SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
 
@@ -212,9 +213,12 @@ class ConvGemmLayer:
 
     def emit(self, prog, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
              ldr: int | None = None, tmp: int | None = None, split: bool | None = None,
-             cfg: int | None = None, opad: int = 0) -> None:
-        """Append this layer's launches to a native Program (or launch now if prog is None)."""
+             cfg: int | None = None, opad: int = 0, pool: dict | None = None) -> None:
+        """Append this layer's launches to a native Program (or launch now if prog is None).
+        ``pool``: fused 3x3/2 max-pool added in the epilogue (MODE_PW only), dict(px, pH, pW,
+        pld, ppad) -- see ConvGemmArgs.px."""
         split = self.split if split is None else split
+        assert pool is None or self.mode == MODE_PW, "the pool epilogue rides a pointwise GEMM"
         cfg = self.cfg if cfg is None else cfg
         C = _lib.lib()
         if self.mode == MODE_DW and split:
@@ -230,6 +234,8 @@ class ConvGemmLayer:
                 prog.add_conv_gemm(self.name, MODE_PW, cfg, ga)
             return
         ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
+        if pool:
+            ga.update(pool)
         if prog is None:
             C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
         else:

@@ -191,6 +191,31 @@ def test_pool_add(H, C, with_res):
     assert err <= 2e-2 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("H,cin,C", [(147, 64, 128), (74, 128, 256), (37, 256, 736), (19, 736, 1024)])
+def test_pointwise_pool_epilogue(H, cin, C):
+    """Residual 1x1/2 conv with the block's TF-'same' 3x3/2 max-pool fused into its epilogue
+    (ConvGemmArgs.px, the Xception "convpool" step) == conv -> pool_add, every tile config."""
+    from kdl.models.layers import tf_same_pad
+    gen = torch.Generator().manual_seed(8)
+    B = 2
+    OH, pt, _ = tf_same_pad(H, 3, 2)
+    lay = _layer(MODE_PW, cin, C, gen, stride=2)
+    assert lay.ldy == C
+    g = Geometry(B, H, H, OH, OH)
+    x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
+    main = torch.randn(B * H * H * C, generator=gen).to(torch.bfloat16).to(DEV)
+    conv = conv_gemm_ref(lay, x, g).to(torch.bfloat16).to(DEV).contiguous()
+    ref = pool_add_ref(main, conv.view(-1), B, H, H, OH, OH, C, pt)
+    pool = dict(px=_lib.ptr(main), pH=H, pW=H, pld=C, ppad=pt)
+    for _, cfg in lay.variants(H):
+        y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lay.check(x, y, g)
+        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=cfg, pool=pool)
+        torch.cuda.synchronize()
+        err = (y.float().view(-1, C) - ref).abs().max().item()
+        assert err <= 2e-2 * ref.abs().max().item(), (cfg, err)
+
+
 def test_head():
     gen = torch.Generator().manual_seed(7)
     B, HW, F_, H1, NC = 5, 100, 2048, 100, 10

@@ -92,7 +92,7 @@ def test_cu_masks_are_disjoint_and_cover():
     assert sum(bin(x).count("1") for x in a + b) == 256
 
 
-def _xception_steps():
+def _xception_steps(fuse=False):
     from kdl.engine import xception as XE
     from kdl.models import xception as X
 
@@ -101,6 +101,7 @@ def _xception_steps():
             self.device = torch.device("cpu")
             self.max_batch, self.buckets, self.steps, self.in_kind = 1, [1], [], "u8"
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
+            self.branches, self.poolfuse = 0, fuse
 
     p = X.init_params(seed=0)
     e = Fake(p)
@@ -135,3 +136,17 @@ def test_resnet_cut_inside_stage_privatises_shared_buffers():
     assert len(sp.boundary) == 1
     # layer3's pad / mid buffers are used on both sides of a layer3.1 cut
     assert "pad14_256#s1" in sp.aliases and "mid14_256#s1" in sp.aliases
+
+
+def test_xception_residual_conv_carries_the_pool():
+    """KDL_POOLFUSE=1: entry/exit blocks lower to residual conv + max-pool as ONE 'convpool' step that reads
+    the block input (src) and the main branch (res) and writes the block output."""
+    steps = _xception_steps(fuse=True)
+    assert not [s for s in steps if s.kind == "pool"]
+    cp = [s for s in steps if s.kind == "convpool"]
+    assert [s.dst for s in cp] == ["block2_out", "block3_out", "block4_out", "block13_out"]
+    assert [s.res for s in cp] == ["block2_sepconv2_out", "block3_sepconv2_out", "block4_sepconv2_out",
+                                   "block13_sepconv2_out"]
+    idx = {s.name: i for i, s in enumerate(steps)}
+    for s in cp:                                  # after the main branch it pools
+        assert idx[s.name] > idx[s.res.replace("_out", "")]
