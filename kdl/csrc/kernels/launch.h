@@ -56,6 +56,11 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);     // ids
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_ws_fits(int cfg, int W);
 int sepconv_fused_config(int cfg, int* bm, int* bn, int* threads);
+// cfg >= C3_CFG_BASE: 3x3 'valid' conv over 2-D tiles with an LDS halo patch (MODE_CONV, cin 32 only,
+// conv3x3_2d.hip: Xception block1_conv2).
+constexpr int C3_CFG_BASE = 208;
+hipError_t conv3x3_2d(int cfg, const ConvGemmArgs& a, hipStream_t s);
+int conv3x3_2d_config(int cfg, int* bm, int* bn, int* threads);
 // cfg >= S2D_CFG_BASE: fused separable conv over 2-D spatial tiles (MODE_DW only, sepconv_2d.hip).
 constexpr int S2D_CFG_BASE = 160;
 hipError_t sepconv_2d(int cfg, const ConvGemmArgs& a, hipStream_t s);

@@ -62,7 +62,11 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            170: (3, 2, 2, 4), 171: (2, 2, 2, 4), 172: (2, 2, 2, 4), 173: (3, 4, 2, 4),
            # persistent 2-D tiled variant (sepconv_2dp_kernel, KDL_S2DP_CONFIGS): weights LDS-resident
            184: (3, 2, 2, 4), 185: (2, 2, 2, 4), 186: (2, 4, 2, 4), 187: (4, 2, 2, 4), 188: (3, 2, 2, 4),
-           189: (2, 4, 2, 4), 190: (2, 2, 2, 4), 191: (2, 2, 2, 4), 192: (3, 2, 2, 4)}
+           189: (2, 4, 2, 4), 190: (2, 2, 2, 4), 191: (2, 2, 2, 4), 192: (3, 2, 2, 4),
+           # 3x3 'valid' conv over 2-D tiles, LDS halo patch, cin 32 (conv3x3_2d.hip, KDL_C3_CONFIGS)
+           208: (2, 2, 4, 2), 209: (1, 2, 4, 2), 210: (2, 2, 4, 2), 211: (3, 2, 4, 2),
+           # ... with a dedicated DMA wave, accumulators stored directly (conv3x3_2dw_kernel)
+           212: (2, 2, 4, 2), 213: (1, 2, 4, 2), 214: (2, 2, 4, 2), 215: (2, 4, 4, 1)}
 # persistent 2-D variant: (STAGES, TH, TW) per id, mirror of KDL_S2DP_CONFIGS (LDS sizing)
 S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188: (6, 6, 16), 189: (4, 4, 16),
         190: (8, 4, 16), 191: (11, 4, 16), 192: (7, 6, 16)}
@@ -70,6 +74,7 @@ SEP_BASE = 64
 SEPP_BASE = 96
 SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
 S2D_BASE = 160    # 2-D spatial tiles (sepconv_2d.hip): the early flow's 147x147 / 74x74 maps
+C3_BASE = 208     # 2-D tiled 3x3 conv, cin 32 (conv3x3_2d.hip): block1_conv2
 S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 48, 19 -> 32)
 # x-band KiB per stage of each KDL_SEPP_CONFIGS entry (mirror of sepconv_pipe_fits)
 SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 104: 12,
@@ -93,6 +98,8 @@ def s2dp_smem(cfg: int, K: int) -> int:
 
 def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | None = None) -> bool:
     """Mirror of the host-side launch checks in sepconv_fused.hip / sepconv_pipe.hip / sepconv_2d.hip."""
+    if cfg >= C3_BASE:    # one N tile of all outputs, 32 input channels (K = 288)
+        return (K is None or K == 288) and (n is None or round_up(n, cfg_tile(cfg)[1]) == cfg_tile(cfg)[1])
     if cfg < SEP_BASE or W is None:
         return True
     if cfg in S2DP:   # one N tile (all of N) with the whole K x N weight block resident in LDS
@@ -122,7 +129,9 @@ def cfg_tile(cfg: int) -> tuple[int, int]:
 def candidate_configs(n: int, m: int | None = None, mode: int | None = None) -> list[int]:
     """Configs whose N tile does not waste more than ~35% of the channels (the fused
     separable ids >= SEP_BASE only for MODE_DW layers)."""
-    ids = sorted(c for c in CONFIGS if c not in ABLATION_IDS and (mode is None or mode == MODE_DW or c < SEP_BASE))
+    ids = sorted(c for c in CONFIGS if c not in ABLATION_IDS
+                 and (mode is None or (c < SEP_BASE) or (mode == MODE_DW and c < C3_BASE)
+                      or (mode == MODE_CONV and c >= C3_BASE)))
     out = [c for c in ids if round_up(n, cfg_tile(c)[1]) <= 1.35 * round_up(n, 16)]
     if not any(c < SEP_BASE for c in out):   # tiny N: always keep the plain GEMMs with the smallest N tile
         plain = [c for c in ids if c < SEP_BASE]
@@ -200,6 +209,9 @@ class ConvGemmLayer:
     def variants(self, W: int | None = None) -> list[tuple[bool, int]]:
         """(split, cfg) pairs valid for this layer (``W``: image width, filters the
         fused separable configs whose LDS row band would not fit)."""
+        if self.mode == MODE_CONV:
+            return [(False, c) for c in self.candidates
+                    if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))]
         if self.mode != MODE_DW:
             return [(False, c) for c in self.candidates if c < SEP_BASE]
         return ([(False, c) for c in self.candidates

@@ -1,8 +1,8 @@
 """Tile-config tables (kdl.ops.conv): what each layer kind may be autotuned over."""
 import pytest
 
-from kdl.ops.conv import (CONFIGS, MODE_CONV, MODE_DW, MODE_PW, S2D_BASE, S2DP, SEP_BASE, candidate_configs,
-                          cfg_tile, config_applicable, s2dp_smem)
+from kdl.ops.conv import (C3_BASE, CONFIGS, MODE_CONV, MODE_DW, MODE_PW, S2D_BASE, S2DP, SEP_BASE,
+                          candidate_configs, cfg_tile, config_applicable, s2dp_smem)
 
 
 @pytest.mark.parametrize("n", [8, 16, 32, 48, 64, 100, 128, 256, 728, 1024, 2048])
@@ -11,8 +11,21 @@ def test_candidates_valid_for_mode(n, mode):
     c = candidate_configs(n, mode=mode)
     assert c, "every layer needs at least one config"
     assert any(x < SEP_BASE for x in c), "a plain GEMM / split path is always available"
-    if mode != MODE_DW:
+    if mode == MODE_PW:
         assert all(x < SEP_BASE for x in c), "fused separable configs are MODE_DW only"
+    if mode == MODE_CONV:
+        assert all(x < SEP_BASE or x >= C3_BASE for x in c), "only the 2-D tiled 3x3 conv joins MODE_CONV"
+    if mode == MODE_DW:
+        assert not any(x >= C3_BASE for x in c)
+
+
+def test_conv3x3_2d_applicability():
+    c3 = [c for c in CONFIGS if c >= C3_BASE]
+    assert c3 and all(cfg_tile(c) == (cfg_tile(c)[0], 64) for c in c3)
+    # Xception block1_conv2: cin 32 (K = 288), 64 outputs
+    assert all(config_applicable(c, 149, 288, 64) for c in c3)
+    assert not any(config_applicable(c, 149, 576, 64) for c in c3)      # cin 64: weights exceed registers
+    assert not any(config_applicable(c, 149, 288, 128) for c in c3)     # more outputs than one N tile
 
 
 def test_2d_configs_tile_shapes():
