@@ -530,6 +530,250 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2dp_kernel(ConvGemmArg
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------
+// Persistent variant with ONE dedicated DMA wave (wave NW) and NW compute waves that
+// store their own accumulators (ids S2DW_OFFSET..; same pattern as conv3x3_2dw_kernel,
+// which took block1_conv2 from 54.5 to 40.4 us). Versus sepconv_2dp_kernel: no C tile in
+// LDS, no storer pass between the epilogue barrier and the next tile, one barrier per
+// k-step, and the compute waves' vmcnt only ever holds their own stores (never waited
+// for in the loop) while the DMA wave's counted wait stays exact. No padded output or
+// transcendental epilogue (the launcher refuses them); a residual is read per lane (8 B).
+template <int FM, int FN, int WGM, int WGN, int STAGES, int TH, int TW, bool RELU>
+__global__ __launch_bounds__(64 * (WGM * WGN + 1)) void sepconv_2dw_kernel(ConvGemmArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
+  static_assert(BM == TH * TW && TW % 16 == 0, "the M tile is TH x TW pixels, 16-pixel row segments");
+  static_assert(NW % 2 == 0 && STAGES >= 3, "a wave's depthwise units share one channel group; ring depth");
+  using P = S2dPatch<TH, TW>;
+  constexpr int AF = BM / 16, BF = BN / 16;
+  constexpr int IPP = P::IPP, XB = P::XB;
+  constexpr int PL = IPP * 1024;
+  constexpr int STAGE = XB * 1024;
+  constexpr int ABUF = AF * 1024;
+  constexpr int U = 2 * AF;
+  constexpr int UPW = (U + NW - 1) / NW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool dma = wave == NW;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int W = a.W, H = a.H;
+  const int KT = a.K >> 5;
+  const int ntw = (W + TW - 1) / TW, nth = (H + TH - 1) / TH;
+  const int ntiles = a.B * nth * ntw;
+  const int G = gridDim.x;
+  const int t0 = xcd_remap(blockIdx.x, G);
+  const int TWn = t0 < ntiles ? (ntiles - t0 + G - 1) / G : 0;
+  const int Q = TWn * KT;
+  if (Q == 0) return;
+  // LDS map: [B resident KT*BF KiB][dw entries KT KiB][ring][A x2]
+  uint8_t* const bres = smem;
+  uint8_t* const dres = smem + KT * BF * 1024;
+  uint8_t* const ring = dres + KT * 1024;
+  uint8_t* const abuf = ring + STAGES * STAGE;
+
+  // resident weights: every wave helps (older than every ring DMA of the DMA wave)
+  for (int idx = wave; idx < KT * BF; idx += NW + 1) {
+    const int k = idx / BF, f = idx - k * BF;
+    glds16(a.wp + ((long)f * KT + k) * 512 + lane * 8, bres + idx * 1024);
+  }
+  for (int k = wave; k < KT; k += NW + 1) glds16((const uint8_t*)a.dwk + k * 1024 + lane * 16, dres + k * 1024);
+
+  if (dma) {
+    // ---- the DMA wave: XB patch instructions per stage, stages in (tile, k) order
+    int iq = 0, ik = 0, iti = 0;
+    const uint8_t* psrc[XB];
+    auto enter_tile = [&](int ti) {
+      const int tile = t0 + ti * G;
+      const int bimg = tile / (nth * ntw), trem = tile - bimg * (nth * ntw);
+      const int h0 = (trem / ntw) * TH, w0 = (trem % ntw) * TW;
+#pragma unroll
+      for (int sidx = 0; sidx < XB; ++sidx) {
+        const int q = sidx / IPP, slot = (sidx % IPP) * 64 + lane;
+        const int pr = slot / P::PW, pc = slot - pr * P::PW;
+        const int h = h0 - 1 + pr, w = w0 - 1 + pc;
+        const bool in = slot < P::PS && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        psrc[sidx] = in ? (const uint8_t*)(a.x + (((long)bimg * H + h) * W + w) * a.ldx + q * 8) : s2d_zeros;
+      }
+    };
+    auto issue = [&](int slotbuf) {
+      uint8_t* base = ring + slotbuf * STAGE;
+#pragma unroll
+      for (int sidx = 0; sidx < XB; ++sidx) glds16(psrc[sidx] + ik * 64, base + sidx * 1024);
+      if (iq + 1 < Q) {
+        ++iq;
+        if (++ik == KT) {
+          ik = 0;
+          enter_tile(++iti);
+        }
+      }
+    };
+    enter_tile(0);
+    for (int p = 0; p < STAGES - 1; ++p) issue(p);
+    s2_wait_barrier<(STAGES - 2) * XB>();       // resident weights + stage 0 landed
+    for (int q = 0; q < Q; ++q) {
+      s2_wait_barrier<(STAGES - 3) * XB>();     // stage q+1 landed
+      issue((q + STAGES - 1) % STAGES);         // slot of stage q-1 (read by the dw of step q-2)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---- compute waves: depthwise units as in sepconv_2d_kernel, pointwise MFMAs, stores
+  const int g = wave & 1;
+  const int p16 = lane & 15, kb = lane >> 4;
+  const int par = kb >> 1;
+  const int qc = 2 * g + (kb & 1);
+  const int ulast = U - 1 - ((U - 1 - wave) & 1);
+  int toff[UPW][5];
+#pragma unroll
+  for (int i = 0; i < UPW; ++i) {
+    const int u = min(wave + NW * i, ulast);
+    const int pix = (u >> 1) * 16 + p16;
+    const int r = pix / TW, c = pix - r * TW;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int tap = 2 * j + par;
+      const int slot = tap < 9 ? (r + tap / 3) * P::PW + c + tap % 3 : P::ZSLOT;
+      toff[i][j] = qc * PL + slot * 16;
+    }
+  }
+  const bool wv = (p16 >> 3) == (kb & 1);
+  const int e = p16 & 7;
+  uint32_t sel[2][4];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t pair = (2u * jp) | ((2u * jp + 1u) << 8);
+      const uint32_t val = (e & 1) ? (0x0c0cu | (pair << 16)) : (0x0c0c0000u | pair);
+      sel[jp][d] = (wv && (e >> 1) == d) ? val : 0x0c0c0c0cu;
+    }
+  const int went = ((g * 16 + p16) * 2 + par) * 16;
+  const int aoffw = (p16 + 16 * (2 * g + (kb >> 1))) * 16 + 8 * (kb & 1);
+  const int quad = lane >> 4, col = lane & 15;
+  float4 bvr[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bvr[j] = *(const float4*)(a.bias + wn * FN * 16 + j * 16 + 4 * quad);
+  int prow[FM], pcol[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int op = (wm * FM + i) * 16 + col;
+    prow[i] = op / TW;
+    pcol[i] = op - prow[i] * TW;
+  }
+
+  auto dw_load = [&](int slotbuf, int k, u32x4 (&xv)[UPW][5]) -> u32x4 {
+    const uint8_t* sb = ring + slotbuf * STAGE;
+#pragma unroll
+    for (int i = 0; i < UPW; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) xv[i][j] = *(const u32x4*)(sb + toff[i][j]);
+    return *(const u32x4*)(dres + k * 1024 + went);
+  };
+  auto dw_mfma = [&](const u32x4 we, u32x4 (&xv)[UPW][5], int ab) {
+    s16x8 wf[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const uint32_t wd = we[j >> 1];
+      u32x4 f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) f[d] = __builtin_amdgcn_perm(wd, wd, sel[j & 1][d]);
+      wf[j] = __builtin_bit_cast(s16x8, f);
+    }
+    f32x4 dacc[UPW];
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) dacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int i = 0; i < UPW; ++i) {
+        u32x4 v = xv[i][j];
+        if constexpr (RELU) {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
+        }
+        dacc[i] = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc[i]);
+      }
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+      const int u = min(wave + NW * i, ulast);
+      *(u32x2*)(abuf + ab * ABUF + (u >> 1) * 1024 + aoffw) =
+          (u32x2){pack_bf16(dacc[i][0], dacc[i][1]), pack_bf16(dacc[i][2], dacc[i][3])};
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  s2_wait_barrier<0>();                         // own weight DMAs + bias loads; DMA wave: stage 0
+  {
+    u32x4 xv[UPW][5];
+    const u32x4 we = dw_load(0, 0, xv);
+    dw_mfma(we, xv, 0);
+  }
+  int k = 0, ti = 0;
+  for (int q = 0; q < Q; ++q) {
+    s2_wait_barrier<63>();                      // A(q) written, stage q+1 landed
+    const uint8_t* As = abuf + (q & 1) * ABUF + lane * 16;
+    const uint8_t* Bs = bres + k * BF * 1024 + lane * 16;
+    s16x8 af[FM], bf[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(As + (wm * FM + i) * 1024);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(Bs + (wn * FN + j) * 1024);
+    const int k1 = k + 1 == KT ? 0 : k + 1;
+    u32x4 xv[UPW][5];
+    const u32x4 we = dw_load((q + 1) % STAGES, k1, xv);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+    dw_mfma(we, xv, (q + 1) & 1);
+    __builtin_amdgcn_s_setprio(0);
+    if (k1 == 0) {
+      // ---- tile epilogue straight from the accumulators (8-byte stores per lane)
+      const int tile = t0 + ti * G;
+      const int bimg = tile / (nth * ntw), trem = tile - bimg * (nth * ntw);
+      const int h0 = (trem / ntw) * TH, w0 = (trem % ntw) * TW;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int h = h0 + prow[i], w = w0 + pcol[i];
+        const bool ok = h < H && w < W;
+        uint16_t* yrow = a.y + ((long)(bimg * H + h) * W + w) * a.ldy;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = wn * FN * 16 + j * 16 + 4 * quad;
+          float v0 = acc[i][j][0] + bvr[j].x, v1 = acc[i][j][1] + bvr[j].y;
+          float v2 = acc[i][j][2] + bvr[j].z, v3 = acc[i][j][3] + bvr[j].w;
+          if (a.relu_out == 1) {
+            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+          }
+          u32x2 o = {pack_bf16(v0, v1), pack_bf16(v2, v3)};
+          if (a.res && ok) {                    // residual (bf16-rounded output + residual, as epi_store)
+            const u32x2 rv = *(const u32x2*)(a.res + ((long)(bimg * H + h) * W + w) * a.ldr + n);
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              o[d] = pack_bf16(bf_lo(o[d]) + bf_lo(rv[d]), bf_hi(o[d]) + bf_hi(rv[d]));
+              if (a.relu_out == 2) o[d] = relu_bf16x2(o[d]);
+            }
+          }
+          if (ok && n < a.nstore) *(u32x2*)(yrow + n) = o;
+          acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      ++ti;
+    }
+    k = k1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // (FM, FN, WGM, WGN, STAGES, TH, TW) of the persistent variant; ids S2D_CFG_BASE + S2DP_OFFSET + i.
 constexpr int S2DP_OFFSET = 24;
 #define KDL_S2DP_CONFIGS(X)     \
@@ -542,6 +786,36 @@ constexpr int S2DP_OFFSET = 24;
   X(6, 2, 2, 2, 4, 8, 4, 16)    \
   X(7, 2, 2, 2, 4, 11, 4, 16)   \
   X(8, 3, 2, 2, 4, 7, 6, 16)
+
+// (FM, FN, WGM, WGN, STAGES, TH, TW) of the DMA-wave variant; ids S2D_CFG_BASE + S2DW_OFFSET + i
+// (host ids 200..207: C3_CFG_BASE = 208 follows).
+constexpr int S2DW_OFFSET = 40;
+#define KDL_S2DW_CONFIGS(X)     \
+  X(0, 2, 2, 2, 4, 4, 4, 16)    \
+  X(1, 4, 2, 2, 4, 4, 8, 16)    \
+  X(2, 3, 2, 2, 4, 4, 6, 16)    \
+  X(3, 2, 4, 2, 4, 4, 4, 16)    \
+  X(4, 4, 2, 2, 4, 6, 8, 16)
+
+static int s2dp_num_cus();
+
+template <int FM, int FN, int WGM, int WGN, int ST, int TH, int TW>
+static hipError_t launch_s2dw(const ConvGemmArgs& a, hipStream_t s) {
+  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN, NT = 64 * (WGM * WGN + 1);
+  using P = S2dPatch<TH, TW>;
+  if (a.NF * 16 != BN || a.px || a.opad || a.relu_out > 2 || a.dt) return hipErrorInvalidValue;
+  const int KT = a.K / 32;
+  const size_t smem = (size_t)KT * (BN / 16) * 1024 + (size_t)KT * 1024 + (size_t)ST * P::XB * 1024 + 2 * (BM / 16) * 1024;
+  if (smem > 160 * 1024) return hipErrorInvalidValue;
+  const int ntiles = a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+  auto kern = a.relu_in ? sepconv_2dw_kernel<FM, FN, WGM, WGN, ST, TH, TW, true>
+                        : sepconv_2dw_kernel<FM, FN, WGM, WGN, ST, TH, TW, false>;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, smem) != hipSuccess || per_cu <= 0) per_cu = 1;
+  const int grid = std::min(ntiles, s2dp_num_cus() * per_cu);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), smem, s, a);
+  return hipGetLastError();
+}
 
 template <int FM, int FN, int WGM, int WGN, int STAGES, int TH, int TW>
 static size_t s2dp_smem(int K) {
@@ -596,6 +870,15 @@ static hipError_t launch_s2dp(const ConvGemmArgs& a, hipStream_t s) {
   X(13, 3, 4, 2, 4, 4, 6, 16)
 
 int sepconv_2d_config(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg >= S2DW_OFFSET) {
+    switch (cfg - S2DW_OFFSET) {
+#define KDL_S2WINFO(id, fm, fn, wgm, wgn, st, th, tw) \
+  case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * (wgm * wgn + 1); return 0;
+      KDL_S2DW_CONFIGS(KDL_S2WINFO)
+#undef KDL_S2WINFO
+      default: return -1;
+    }
+  }
   if (cfg >= S2DP_OFFSET) {
     switch (cfg - S2DP_OFFSET) {
 #define KDL_S2PINFO(id, fm, fn, wgm, wgn, st, th, tw) \
@@ -619,6 +902,15 @@ hipError_t sepconv_2d(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (sepconv_2d_config(cfg, &bm, &bn, &th) != 0 || a.K % 32 != 0 || a.K > 8192 || (a.NF * 16) % bn != 0 ||
       a.OH != a.H || a.OW != a.W || a.M != a.B * a.H * a.W || a.M <= 0 || a.dwk == nullptr)
     return hipErrorInvalidValue;
+  if (cfg >= S2DW_OFFSET) {
+    switch (cfg - S2DW_OFFSET) {
+#define KDL_S2WCASE(id, fm, fn, wgm, wgn, st, th, tw) \
+  case id: return launch_s2dw<fm, fn, wgm, wgn, st, th, tw>(a, s);
+      KDL_S2DW_CONFIGS(KDL_S2WCASE)
+#undef KDL_S2WCASE
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (cfg >= S2DP_OFFSET) {
     switch (cfg - S2DP_OFFSET) {
 #define KDL_S2PCASE(id, fm, fn, wgm, wgn, st, th, tw) \

@@ -63,6 +63,8 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            # persistent 2-D tiled variant (sepconv_2dp_kernel, KDL_S2DP_CONFIGS): weights LDS-resident
            184: (3, 2, 2, 4), 185: (2, 2, 2, 4), 186: (2, 4, 2, 4), 187: (4, 2, 2, 4), 188: (3, 2, 2, 4),
            189: (2, 4, 2, 4), 190: (2, 2, 2, 4), 191: (2, 2, 2, 4), 192: (3, 2, 2, 4),
+           # persistent 2-D sepconv with a dedicated DMA wave, direct stores (KDL_S2DW_CONFIGS)
+           200: (2, 2, 2, 4), 201: (4, 2, 2, 4), 202: (3, 2, 2, 4), 203: (2, 4, 2, 4), 204: (4, 2, 2, 4),
            # 3x3 'valid' conv over 2-D tiles, LDS halo patch, cin 32 (conv3x3_2d.hip, KDL_C3_CONFIGS)
            208: (2, 2, 4, 2), 209: (1, 2, 4, 2), 210: (2, 2, 4, 2), 211: (3, 2, 4, 2),
            # ... with a dedicated DMA wave, accumulators stored directly (conv3x3_2dw_kernel)
@@ -70,6 +72,8 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
 # persistent 2-D variant: (STAGES, TH, TW) per id, mirror of KDL_S2DP_CONFIGS (LDS sizing)
 S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188: (6, 6, 16), 189: (4, 4, 16),
         190: (8, 4, 16), 191: (11, 4, 16), 192: (7, 6, 16)}
+# DMA-wave variant (sepconv_2dw_kernel): no C tile / bias in LDS
+S2DW = {200: (4, 4, 16), 201: (4, 8, 16), 202: (4, 6, 16), 203: (4, 4, 16), 204: (6, 8, 16)}
 SEP_BASE = 64
 SEPP_BASE = 96
 SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
@@ -88,11 +92,13 @@ SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6,
 
 
 def s2dp_smem(cfg: int, K: int) -> int:
-    """LDS bytes of a persistent 2-D sepconv config (mirror of s2dp_smem in sepconv_2d.hip)."""
-    st, th, tw = S2DP[cfg]
+    """LDS bytes of a persistent 2-D sepconv config (mirror of s2dp_smem / launch_s2dw in sepconv_2d.hip)."""
+    st, th, tw = S2DP[cfg] if cfg in S2DP else S2DW[cfg]
     bm, bn = cfg_tile(cfg)
     ipp = ((th + 2) * (tw + 2) + 1 + 63) // 64
     kt = K // 32
+    if cfg in S2DW:
+        return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024
     return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024 + bm * (bn * 2 + 16) + 1024
 
 
@@ -102,7 +108,7 @@ def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | No
         return (K is None or K == 288) and (n is None or round_up(n, cfg_tile(cfg)[1]) == cfg_tile(cfg)[1])
     if cfg < SEP_BASE or W is None:
         return True
-    if cfg in S2DP:   # one N tile (all of N) with the whole K x N weight block resident in LDS
+    if cfg in S2DP or cfg in S2DW:   # one N tile (all of N) with the whole K x N weight block resident in LDS
         return (W >= S2D_MIN_W and (K is None or s2dp_smem(cfg, K) <= 160 * 1024)
                 and (n is None or round_up(n, cfg_tile(cfg)[1]) == cfg_tile(cfg)[1]))
     if cfg >= S2D_BASE:

@@ -1,7 +1,7 @@
 """Tile-config tables (kdl.ops.conv): what each layer kind may be autotuned over."""
 import pytest
 
-from kdl.ops.conv import (C3_BASE, CONFIGS, MODE_CONV, MODE_DW, MODE_PW, S2D_BASE, S2DP, SEP_BASE,
+from kdl.ops.conv import (C3_BASE, CONFIGS, MODE_CONV, MODE_DW, MODE_PW, S2D_BASE, S2DP, S2DW, SEP_BASE,
                           candidate_configs, cfg_tile, config_applicable, s2dp_smem)
 
 
@@ -44,6 +44,10 @@ def test_persistent_lds_budget():
     assert all(s2dp_smem(cfg, 64) < s2dp_smem(cfg, 128) for cfg in S2DP)
     # too narrow a map for 16-pixel tile rows
     assert not any(config_applicable(cfg, 37, 128, 128) for cfg in S2DP)
+    # the DMA-wave variant keeps no C tile / bias in LDS: strictly smaller than its 2dp twin
+    assert s2dp_smem(201, 128) < s2dp_smem(187, 128)
+    assert all(config_applicable(cfg, 147, 128, cfg_tile(cfg)[1]) for cfg in S2DW)
+    assert not any(config_applicable(cfg, 147, 736, cfg_tile(cfg)[1]) for cfg in S2DW)
 
 
 def test_lanes_hw_queue_budget(monkeypatch):
