@@ -43,6 +43,7 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.dt = I(d, "dt");
   a.px = P<const uint16_t>(d, "px");
   a.pH = I(d, "pH"); a.pW = I(d, "pW"); a.pld = I(d, "pld"); a.ppad = I(d, "ppad");
+  a.wimg = I(d, "wimg");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {
@@ -127,6 +128,12 @@ ChScaleArgs chs_args(const py::dict& d) {
   ChScaleArgs a{};
   a.y = P<uint16_t>(d, "y"); a.scale = P<const float>(d, "scale");
   a.B = I(d, "B"); a.HW = I(d, "HW"); a.C = I(d, "C");
+  return a;
+}
+WScaleArgs ws_args(const py::dict& d) {
+  WScaleArgs a{};
+  a.w = P<const uint16_t>(d, "w"); a.scale = P<const float>(d, "scale"); a.y = P<uint16_t>(d, "y");
+  a.B = I(d, "B"); a.NF = I(d, "NF"); a.KT = I(d, "KT"); a.C = I(d, "C");
   return a;
 }
 GemmF8Args f8_args(const py::dict& d) {
@@ -275,6 +282,11 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(channel_scale(a, S(s)), "channel_scale");
   });
+  m.def("weight_scale", [](py::dict d, uintptr_t s) {
+    const auto a = ws_args(d);
+    py::gil_scoped_release nogil;
+    chk(weight_scale(a, S(s)), "weight_scale");
+  });
   m.def("gemm_f8", [](int cfg, py::dict d, uintptr_t s) {
     const auto a = f8_args(d);
     py::gil_scoped_release nogil;
@@ -343,6 +355,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_se", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_SE; op.name = name; op.se = se_args(d); p.add(op);
+      })
+      .def("add_wscale", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_WSCALE; op.name = name; op.ws = ws_args(d); p.add(op);
       })
       .def("add_chscale", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_CHSCALE; op.name = name; op.cs = chs_args(d); p.add(op);

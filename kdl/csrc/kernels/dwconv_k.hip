@@ -224,16 +224,14 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- squeeze-excite
-// grid (image, 256-channel slice): every block re-sums the tiles' fc1 parts (tiny),
-// applies bias + SiLU, then its 256 channels run fc2 with the TRANSPOSED w2 ([Cs][C]:
-// coalesced across threads, independent loads) and the sigmoid.
-// One workgroup per image. The tile partials of the fused pool (ntiles x Cs floats) are
-// summed by all 256 threads: G = 256 / Cs thread groups each sum every G-th tile of
-// every unit in a fixed order, then one thread per unit adds the G group sums in order
-// (deterministic: atomics would make the sums order-dependent, and 55 blocks of SiLU
-// amplify that run-to-run). The previous form looped over the tiles serially in Cs
-// threads and recomputed that sum in every channel block of the grid, ~35 us per call
-// on B7 (8 % of the forward) for a few hundred thousand MACs.
+// grid (image, 256-channel slice). Each workgroup sums the tile partials of the fused
+// pool (ntiles x Cs floats) with all 256 threads: G = 256 / Cs thread groups each sum
+// every G-th tile of every unit in a fixed order, then one thread per unit adds the G
+// group sums in order (deterministic: atomics would make the sums order-dependent, and
+// 55 blocks of SiLU amplify that run-to-run); bias + SiLU; then its 256 channels run fc2
+// with the TRANSPOSED w2 ([Cs][C]: coalesced across threads) and the sigmoid. The first
+// form summed the tiles serially in Cs threads (~35 us per call on B7); one workgroup
+// per image then left the 3840 x 160 fc2 of the late stages on 32 CUs.
 __global__ __launch_bounds__(256) void se_kernel(SeArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];   // [256] group sums, [Cs] hidden
   float* part = sm;
@@ -261,7 +259,11 @@ __global__ __launch_bounds__(256) void se_kernel(SeArgs a) {
     hid[j] = silu(h * inv + a.b1[j]);
   }
   __syncthreads();
-  for (int c = tid; c < a.C; c += 256) {
+  // fc2 for this workgroup's 256-channel slice (grid.y): the hidden vector above is
+  // recomputed per slice (ntiles x Cs adds, cheap), so the C x Cs fc2 of the wide late
+  // stages (3840 x 160) spreads over C/256 workgroups per image instead of one
+  const int c = blockIdx.y * 256 + tid;
+  if (c < a.C) {
     float s = a.b2[c];
 #pragma unroll 8
     for (int j = 0; j < a.Cs; ++j) s += a.w2t[(long)j * a.C + c] * hid[j];
@@ -270,9 +272,9 @@ __global__ __launch_bounds__(256) void se_kernel(SeArgs a) {
 }
 
 hipError_t squeeze_excite(const SeArgs& a, hipStream_t s) {
-  if (a.B <= 0 || a.Cs <= 0 || a.ntiles <= 0) return hipErrorInvalidValue;
+  if (a.B <= 0 || a.Cs <= 0 || a.ntiles <= 0 || a.C <= 0 || a.B > 65535) return hipErrorInvalidValue;
   const size_t smem = (size_t)(256 + a.Cs) * sizeof(float);
-  hipLaunchKernelGGL(se_kernel, dim3(a.B), dim3(256), smem, s, a);
+  hipLaunchKernelGGL(se_kernel, dim3(a.B, (a.C + 255) / 256), dim3(256), smem, s, a);
   return hipGetLastError();
 }
 
@@ -301,6 +303,38 @@ hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   const dim3 grid((unsigned)(((long)a.HW * (a.C / 8) + 255) / 256), (unsigned)a.B);
   hipLaunchKernelGGL(chscale_kernel, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- SE scale -> weights
+// Folding the squeeze-excite scale into the project conv: (D * s_b) W^T = D (W * s_b)^T, so
+// instead of rewriting the whole depthwise output D in place (chscale: read + write of the
+// largest tensors of the network) each image gets its own copy of the packed project
+// weights scaled along k -- N x K per image, ~1000x fewer bytes in the early stages.
+// One thread = one 16-byte lane slot (8 consecutive k of one output channel).
+__global__ __launch_bounds__(256) void wscale_kernel(WScaleArgs a) {
+  const long per = (long)a.NF * a.KT * 64;     // 16-byte slots per image
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= per) return;
+  const int b = blockIdx.y;
+  const int lane = (int)(i & 63);
+  const int t = (int)((i >> 6) % a.KT);
+  const int k0 = t * 32 + (lane >> 4) * 8;
+  const float4* sc = (const float4*)(a.scale + (long)b * a.C + k0);
+  const float4 s0 = sc[0], s1 = sc[1];
+  u32x4 v = *(const u32x4*)(a.w + i * 8);
+  v[0] = pack_bf16(bf_lo(v[0]) * s0.x, bf_hi(v[0]) * s0.y);
+  v[1] = pack_bf16(bf_lo(v[1]) * s0.z, bf_hi(v[1]) * s0.w);
+  v[2] = pack_bf16(bf_lo(v[2]) * s1.x, bf_hi(v[2]) * s1.y);
+  v[3] = pack_bf16(bf_lo(v[3]) * s1.z, bf_hi(v[3]) * s1.w);
+  *(u32x4*)(a.y + ((long)b * per + i) * 8) = v;
+}
+
+hipError_t weight_scale(const WScaleArgs& a, hipStream_t s) {
+  if (a.B <= 0 || a.B > 65535 || a.NF <= 0 || a.KT <= 0 || a.C < 32 * a.KT || a.C % 4 != 0)
+    return hipErrorInvalidValue;
+  const long per = (long)a.NF * a.KT * 64;
+  hipLaunchKernelGGL(wscale_kernel, dim3((unsigned)((per + 255) / 256), (unsigned)a.B), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

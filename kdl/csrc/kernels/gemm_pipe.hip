@@ -57,13 +57,23 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WGN, wn = wave % WGN;
   const int nN = (a.NF * 16) / BN;
-  const int nM = (a.M + BM - 1) / BM;
+  const int OHW = a.OH * a.OW;
+  // per-image weights (a.wimg): M tiles are cut per image so a tile has one weight set
+  const int mpi = a.wimg ? (OHW + BM - 1) / BM : 0;
+  const int nM = a.wimg ? a.B * mpi : (a.M + BM - 1) / BM;
   const int wg = xcd_remap(blockIdx.x, nM * nN);
   const int mi = wg / nN, ni = wg % nN;
-  const int m0 = mi * BM, n0 = ni * BN;
+  int m0 = mi * BM, mend = a.M;
+  long wofs = 0;
+  if (a.wimg) {
+    const int bi = mi / mpi;
+    m0 = bi * OHW + (mi - bi * mpi) * BM;
+    mend = (bi + 1) * OHW;
+    wofs = (long)bi * a.wimg;
+  }
+  const int n0 = ni * BN;
   const int KT32 = a.K >> 5;                  // 32-deep k steps
   const int KT = (KT32 + KSUB - 1) / KSUB;    // pipeline stages
-  const int OHW = a.OH * a.OW;
 
   // per-lane source offsets of the fragments this wave stages
   long src[L];
@@ -72,14 +82,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     const int f = min(wave + i * NW, FR - 1);
     if (f < AF) {
       int m = m0 + f * 16 + (lane & 15);
-      m = m < a.M ? m : a.M - 1;
+      m = m < mend ? m : mend - 1;
       const int b = m / OHW, rem = m - b * OHW;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       const long pix = ((long)b * a.H + (long)oh * a.stride) * a.W + (long)ow * a.stride;
       src[i] = pix * a.ldx + 8 * (lane >> 4);
     } else {
       const int nf = n0 / 16 + (f - AF);
-      src[i] = ((long)nf * KT32) * 512 + lane * 8;
+      src[i] = wofs + ((long)nf * KT32) * 512 + lane * 8;
     }
   }
 
@@ -195,7 +205,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   for (int c = tid; c < BM * CPR; c += 64 * NW) {
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
-    if (m < a.M && n < a.nstore) {
+    if (m < mend && n < a.nstore) {
       if constexpr (ABL & 4) {
         if (smem[r * CS + cc * 16] == 0x7f && smem[r * CS + cc * 16 + 1] == 0x7f) a.y[0] = 1;   // keep the tile live
       } else {
@@ -260,7 +270,8 @@ template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int ABL = 
 static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
-  const int nM = (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
+  if (a.wimg && (a.M != a.B * a.OH * a.OW || a.B <= 0)) return hipErrorInvalidValue;
+  const int nM = a.wimg ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
   hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, ABL, DT>), dim3(nM * nN),
                      dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();

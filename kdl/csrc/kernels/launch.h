@@ -39,6 +39,10 @@ struct ConvGemmArgs {
   // conv result never round-trips through HBM (epilogue.h)
   const uint16_t* px;
   int pH, pW, pld, ppad;
+  // per-image weights (EfficientNet project conv with the SE channel scale folded in, gemm_pipe
+  // only): wp points at [B][NF][K/32][64][8] and wimg is the element stride between images;
+  // M tiles then never straddle two images. 0 = one weight set for every row.
+  int wimg;
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
@@ -222,6 +226,16 @@ struct ChScaleArgs {
   int B, HW, C;
 };
 hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s);
+
+// SE scale folded into the project conv's weights: y[b] = w * scale[b][k] for every element of
+// the packed fragments w [NF][KT][64][8] (k = 32 t + 8 (lane >> 4) + e), bf16.
+struct WScaleArgs {
+  const uint16_t* w;      // [NF][KT][64][8]
+  const float* scale;     // [B][C]
+  uint16_t* y;            // [B][NF][KT][64][8]
+  int B, NF, KT, C;       // C: scale row stride (>= 32 KT)
+};
+hipError_t weight_scale(const WScaleArgs& a, hipStream_t s);
 
 // FP8 (OCP e4m3) GEMM, gemm_f8.hip: y = act(colscale[n] * A8 W8^T + bias[n]) (+res), bf16 or fp8 out.
 struct GemmF8Args {

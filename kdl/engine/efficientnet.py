@@ -9,8 +9,10 @@ Lowering (captured into one hipGraph per batch bucket):
       dwk           KxK/S depthwise + BN + SiLU; SE average pool + squeeze FC fused
                     (per-tile partials of fc1, which is linear in the pooled mean)
       se            SE tail: sum parts + bias + SiLU, fc2 + sigmoid -> per-(image, channel) scale
-      chscale       depthwise output *= SE scale (in place)
-      conv_gemm PW  project 1x1 + BN (+ identity residual)
+      wscale        SE scale folded into per-image copies of the project weights (N x K per
+                    image) instead of rewriting the depthwise output in place (chscale: a
+                    read + write of the largest tensors; KDL_SEFOLD=0 restores it)
+      conv_gemm PW  project 1x1 + BN (+ identity residual), per-image weights
     conv_gemm PW    head 1x1 640 -> 2560 + BN + SiLU
     gap + fc_mfma   global pool (bf16) -> classifier 2560 -> 1000
 
@@ -20,13 +22,14 @@ largest tensor (stage-2 expand at 300x300x192) is 34.6 MB per image, so at batch
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 
 import torch
 
 from ..models import efficientnet as E
 from ..ops import _lib
-from ..ops.conv import MODE_PW, ConvGemmLayer, Geometry
+from ..ops.conv import MODE_PW, PIPE_BASE, SEP_BASE, ConvGemmLayer, Geometry, default_config
 from ..ops.pack import pack_fragments, round_up
 from .base import EngineBase, Step
 
@@ -45,6 +48,8 @@ class EfficientNetEngine(EngineBase):
                  buckets=None, tune_file: str | Path | None = None, size: int = E.INPUT_SIZE):
         super().__init__(device, max_batch, buckets)
         self.size = size
+        self.sefold = os.environ.get("KDL_SEFOLD", "1") != "0"
+        self.wimg_max = 0                          # largest packed project weight set (elements)
         self.classes = params["classifier.1.bias"].numel()
         self.bufsz: dict[str, int] = {}            # buffer -> elements per image (max over uses)
         self._build(params)
@@ -96,14 +101,25 @@ class EfficientNetEngine(EngineBase):
                                    p[f"{se}.fc2.bias"].float().to(dev))
             self.steps.append(Step("se", f"{blk.prefix}.se", src="pool", dst="scale", geom=(H, H, oh, oh),
                                    extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
-            # in place on D (src == dst); reads the SE scales
-            self.steps.append(Step("chscale", f"{blk.prefix}.scale", src="D", dst="D", res="scale",
-                                   geom=(oh, oh, oh, oh), extra=dict(C=ce)))
             ping ^= 1
             out = f"X{ping}"
             lay = self._pw(n["project"], p, f"{n['project']}.0.weight", f"{n['project']}.1", ce, blk.cout, 0)
+            if self.sefold:
+                # the SE scale goes into per-image copies of the project weights ("wimg",
+                # scratch), consumed by the LDS-DMA GEMM with per-image M tiles
+                lay.candidates = [c for c in lay.candidates if PIPE_BASE <= c < SEP_BASE]
+                if lay.cfg not in lay.candidates:
+                    lay.cfg = default_config(MODE_PW, blk.cout, 0) if default_config(MODE_PW, blk.cout, 0) in \
+                        lay.candidates else lay.candidates[0]
+                self.wimg_max = max(self.wimg_max, lay.wp.numel())
+                self.steps.append(Step("wscale", f"{blk.prefix}.wscale", src="scale", dst="wimg",
+                                       geom=(oh, oh, oh, oh), extra=dict(C=ce, layer=lay)))
+            else:
+                # in place on D (src == dst); reads the SE scales
+                self.steps.append(Step("chscale", f"{blk.prefix}.scale", src="D", dst="D", res="scale",
+                                       geom=(oh, oh, oh, oh), extra=dict(C=ce)))
             self.steps.append(Step("conv", lay.name, lay, "D", out, res=cur if blk.residual else None,
-                                   geom=(oh, oh, oh, oh), extra=dict(ldx=ce, ldr=ldc)))
+                                   geom=(oh, oh, oh, oh), extra=dict(ldx=ce, ldr=ldc, wimg=self.sefold)))
             self._need(out, oh * oh * lay.ldy)
             cur, ldc, H = out, lay.ldy, oh
         lay = self._pw("features.8", p, "features.8.0.weight", "features.8.1", E.blocks()[-1].cout, E.HEAD, 4)
@@ -137,6 +153,8 @@ class EfficientNetEngine(EngineBase):
         self.feat = torch.zeros(((B + 15) // 16 * 16, E.HEAD), dtype=torch.bfloat16, device=dev)
         # by name, so stages.py can version / privatise them like the activations
         self.bufs.update(pool=self.pool, scale=self.scale, feat=self.feat)
+        if self.wimg_max:
+            self.bufs["wimg"] = torch.zeros(B * self.wimg_max, dtype=torch.bfloat16, device=dev)
         self.logits = torch.zeros((B, self.classes), dtype=torch.float32, device=dev)
 
     def _ptr(self, name: str) -> int:
@@ -147,13 +165,14 @@ class EfficientNetEngine(EngineBase):
     def scratch_buffers(self) -> list[str]:
         """SE partial pools (written by the dw kernel, not a step dst) and scales: used
         within one block, so each pipeline stage gets its own (stages.py)."""
-        return ["pool", "scale"]
+        return ["pool", "scale", "wimg"] if self.wimg_max else ["pool", "scale"]
 
     def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
         H, W, OH, OW = step.geom
+        wimg = (self._ptr("wimg"), step.layer.wp.numel()) if step.extra.get("wimg") else None
         step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
                         res=self._ptr(step.res) if step.res else None, ldx=step.extra["ldx"],
-                        ldr=step.extra.get("ldr") if step.res else None, split=False, cfg=cfg)
+                        ldr=step.extra.get("ldr") if step.res else None, split=False, cfg=cfg, wimg=wimg)
 
     def _emit(self, prog, step: Step, b: int) -> None:
         H, W, OH, OW = step.geom if step.geom else (0, 0, 0, 0)
@@ -181,6 +200,10 @@ class EfficientNetEngine(EngineBase):
                                         w2t=_lib.ptr(w2t), b2=_lib.ptr(b2), scale=self._ptr("scale"), B=b,
                                         ntiles=self.ntiles[step.extra["blk"]], HW=OH * OW, C=step.extra["C"],
                                         Cs=step.extra["Cs"]))
+        elif step.kind == "wscale":
+            lay = step.extra["layer"]
+            prog.add_wscale(step.name, dict(w=_lib.ptr(lay.wp), scale=self._ptr("scale"), y=self._ptr("wimg"),
+                                            B=b, NF=lay.nf_max, KT=lay.K // 32, C=step.extra["C"]))
         elif step.kind == "chscale":
             prog.add_chscale(step.name, dict(y=self._ptr("D"), scale=self._ptr("scale"), B=b, HW=OH * OW,
                                              C=step.extra["C"]))

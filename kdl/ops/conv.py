@@ -231,10 +231,12 @@ class ConvGemmLayer:
 
     def emit(self, prog, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
              ldr: int | None = None, tmp: int | None = None, split: bool | None = None,
-             cfg: int | None = None, opad: int = 0, pool: dict | None = None) -> None:
+             cfg: int | None = None, opad: int = 0, pool: dict | None = None,
+             wimg: tuple[int, int] | None = None) -> None:
         """Append this layer's launches to a native Program (or launch now if prog is None).
         ``pool``: fused 3x3/2 max-pool added in the epilogue (MODE_PW only), dict(px, pH, pW,
-        pld, ppad) -- see ConvGemmArgs.px."""
+        pld, ppad) -- see ConvGemmArgs.px. ``wimg``: (pointer, per-image element stride) of
+        per-image copies of the packed weights (ConvGemmArgs.wimg; LDS-DMA GEMM configs only)."""
         split = self.split if split is None else split
         assert pool is None or self.mode == MODE_PW, "the pool epilogue rides a pointwise GEMM"
         cfg = self.cfg if cfg is None else cfg
@@ -254,6 +256,9 @@ class ConvGemmLayer:
         ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
         if pool:
             ga.update(pool)
+        if wimg:
+            assert PIPE_BASE <= cfg < SEP_BASE, "per-image weights ride the LDS-DMA pipelined GEMM"
+            ga.update(wp=wimg[0], wimg=wimg[1])
         if prog is None:
             C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
         else:

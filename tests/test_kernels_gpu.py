@@ -216,6 +216,36 @@ def test_pointwise_pool_epilogue(H, cin, C):
         assert err <= 2e-2 * ref.abs().max().item(), (cfg, err)
 
 
+@pytest.mark.parametrize("HW,K,N", [(37 * 37, 480, 80), (19 * 19, 2304, 384), (150 * 150 // 9, 288, 48)])
+def test_per_image_weights_fold_channel_scale(HW, K, N):
+    """EfficientNet SE fold: weight_scale makes per-image copies of the packed project weights
+    scaled along k; the LDS-DMA GEMM with ConvGemmArgs.wimg (per-image M tiles) must equal
+    (D * s_b) W^T, every pipelined tile config."""
+    from kdl.ops.conv import PIPE_BASE, SEP_BASE
+    gen = torch.Generator().manual_seed(9)
+    B = 3
+    lay = _layer(MODE_PW, K, N, gen)
+    g = Geometry(B, HW, 1, HW, 1)
+    x = _rand_act((B, HW, 1), lay.cin_pad, K, gen)
+    sc = (torch.rand(B, K, generator=gen) + 0.25).to(DEV)
+    xs = (x.float().view(B, HW, lay.cin_pad) * sc[:, None, :]).to(torch.bfloat16).contiguous()
+    ref = conv_gemm_ref(lay, xs.view(-1), g)
+    per = lay.wp.numel()
+    wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
+    _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B, NF=lay.nf_max,
+                                 KT=lay.K // 32, C=K), _lib.stream_ptr())
+    cfgs = [c for _, c in lay.variants(1) if PIPE_BASE <= c < SEP_BASE]
+    assert cfgs
+    for cfg in cfgs:
+        y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=cfg, wimg=(_lib.ptr(wimg), per))
+        torch.cuda.synchronize()
+        try:
+            _check(y, ref, N, tol=3e-2)
+        except AssertionError as e:
+            raise AssertionError(f"cfg={cfg}: {e}") from None
+
+
 def test_head():
     gen = torch.Generator().manual_seed(7)
     B, HW, F_, H1, NC = 5, 100, 2048, 100, 10
