@@ -209,6 +209,23 @@ struct DwkArgs {
 hipError_t dwk(const DwkArgs& a, hipStream_t s);
 void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles);
 
+// Fused MBConv front half (mbconv.hip): expand 1x1 + BN + SiLU -> KxK/S depthwise + BN + SiLU
+// -> SE pool / fc1 partials, the expanded tensor staying in LDS.
+struct MbedArgs {
+  const uint16_t* x;      // [B][H][W][ldx] block input
+  const uint16_t* we;     // expand weights, packed fragments [C/16 (+pad)][cin/32][64][8]
+  const float* be;        // [C] expand bias
+  const float* wd;        // [K*K][C] depthwise weights fp32 (BN folded)
+  const float* bd;        // [C] depthwise bias
+  uint16_t* y;            // [B][OH][OW][C] depthwise output
+  float* pool;            // [B][ntiles][Cs] fc1 partials
+  const float* w1;        // [Cs][C]
+  int B, H, W, ldx, cin, C, OH, OW, K, S, pad, Cs;
+  int abl;                // timing ablations (tools only): 1 no depthwise, 2 no expand MFMA, 4 no reductions
+};
+hipError_t mbconv_ed(const MbedArgs& a, hipStream_t s);
+void mbconv_ed_tiles(const MbedArgs& a, int* rb, int* tw, int* ntiles);
+
 // Squeeze-excite tail: scale[b][c] = sigmoid(W2 SiLU(sum_parts pool / HW + b1) + b2).
 struct SeArgs {
   const float* pool;      // [B][ntiles][Cs] fc1 partials from dwk

@@ -5,6 +5,9 @@ Lowering (captured into one hipGraph per batch bucket):
 
     stem_conv       3x3/2 pad 1, 3 -> 64 + BN + SiLU, mean/std applied on load
     per MBConv (55):
+      mbconv_ed     expand 1x1 + BN + SiLU -> KxK/S depthwise + BN + SiLU -> SE pool/fc1
+                    partials in ONE kernel, the expanded tensor kept in LDS (mbconv.hip;
+                    expand-ratio-6 blocks with cin <= 160: stages 2-4; KDL_MBED=1), else
       conv_gemm PW  expand 1x1 + BN + SiLU                  (expand ratio 6 blocks)
       dwk           KxK/S depthwise + BN + SiLU; SE average pool + squeeze FC fused
                     (per-tile partials of fc1, which is linear in the pooled mean)
@@ -49,6 +52,10 @@ class EfficientNetEngine(EngineBase):
         super().__init__(device, max_batch, buckets)
         self.size = size
         self.sefold = os.environ.get("KDL_SEFOLD", "1") != "0"
+        # fused expand + depthwise (mbconv.hip): off by default until it beats the unfused pair
+        # (first cut: 926 vs 1800 img/s -- per 32-channel block the workgroup waited a full
+        # memory round trip for the next block's parameters; profiles/entry_flow_r2.txt)
+        self.mbed = os.environ.get("KDL_MBED", "0") == "1"
         self.wimg_max = 0                          # largest packed project weight set (elements)
         self.classes = params["classifier.1.bias"].numel()
         self.bufsz: dict[str, int] = {}            # buffer -> elements per image (max over uses)
@@ -77,28 +84,40 @@ class EfficientNetEngine(EngineBase):
         self.steps.append(Step("stem", "stem", src="input", dst="X0", geom=(self.size, self.size, H, H)))
         self._need("X0", H * H * E.STEM)
         cur, ldc, ping = "X0", E.STEM, 0
-        self.dw, self.se = {}, {}
+        self.dw, self.se, self.expand = {}, {}, {}
+        C = _lib.lib()
         for blk in E.blocks():
             n = blk.names()
             ce = blk.cexp
             oh = (H + 2 * ((blk.k - 1) // 2) - blk.k) // blk.stride + 1
             src = cur
-            if "expand" in n:
-                lay = self._pw(n["expand"], p, f"{n['expand']}.0.weight", f"{n['expand']}.1", blk.cin, ce, 4)
-                self.steps.append(Step("conv", lay.name, lay, cur, "E", geom=(H, H, H, H), extra=dict(ldx=ldc)))
-                self._need("E", H * H * ce)
-                src = "E"
             wd, sd, td = _fold(p, f"{n['dw']}.0.weight", f"{n['dw']}.1")
             dww = (wd[:, 0] * sd[:, None, None]).permute(1, 2, 0).reshape(blk.k * blk.k, ce)
             self.dw[blk.prefix] = (dww.float().contiguous().to(dev), td.float().to(dev))
-            self.steps.append(Step("dwk", f"{blk.prefix}.dw", src=src, dst="D", geom=(H, H, oh, oh),
-                                   extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
-            self._need("D", oh * oh * ce)
             se = n["se"]
             self.se[blk.prefix] = (p[f"{se}.fc1.weight"].reshape(blk.csq, ce).float().contiguous().to(dev),
                                    p[f"{se}.fc1.bias"].float().to(dev),
                                    p[f"{se}.fc2.weight"].reshape(ce, blk.csq).t().float().contiguous().to(dev),
                                    p[f"{se}.fc2.bias"].float().to(dev))
+            geo = dict(B=1, H=H, W=H, ldx=ldc, C=ce, OH=oh, OW=oh, K=blk.k, S=blk.stride,
+                       pad=(blk.k - 1) // 2, Cs=blk.csq)
+            fused = False
+            if "expand" in n:
+                lay = self._pw(n["expand"], p, f"{n['expand']}.0.weight", f"{n['expand']}.1", blk.cin, ce, 4)
+                fused = self.mbed and C.mbconv_ed_tiles(dict(geo, cin=lay.cin_pad))[2] > 0
+                if fused:
+                    self.expand[blk.prefix] = lay
+                    self.steps.append(Step("mbed", f"{blk.prefix}.mbed", src=cur, dst="D", geom=(H, H, oh, oh),
+                                           extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix,
+                                                      ldx=ldc, cin=lay.cin_pad)))
+                else:
+                    self.steps.append(Step("conv", lay.name, lay, cur, "E", geom=(H, H, H, H), extra=dict(ldx=ldc)))
+                    self._need("E", H * H * ce)
+                    src = "E"
+            if not fused:
+                self.steps.append(Step("dwk", f"{blk.prefix}.dw", src=src, dst="D", geom=(H, H, oh, oh),
+                                       extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
+            self._need("D", oh * oh * ce)
             self.steps.append(Step("se", f"{blk.prefix}.se", src="pool", dst="scale", geom=(H, H, oh, oh),
                                    extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
             ping ^= 1
@@ -132,14 +151,17 @@ class EfficientNetEngine(EngineBase):
         self.fc_b = p["classifier.1.bias"].float().to(dev)
         self.steps.append(Step("fc", "classifier", src="feat", dst="logits"))
         # SE pooling partials: ntiles of each dw launch (host mirror of the kernel's tiling)
-        C = _lib.lib()
         self.ntiles = {}
         mx = 1
         for st in self.steps:
-            if st.kind == "dwk":
+            if st.kind in ("dwk", "mbed"):
                 H_, W_, oh_, ow_ = st.geom
-                nt = C.dwk_tiles(dict(B=1, H=H_, W=W_, C=st.extra["C"], OH=oh_, OW=ow_, K=st.extra["K"],
-                                      S=st.extra["S"], pad=(st.extra["K"] - 1) // 2))[3]
+                g = dict(B=1, H=H_, W=W_, C=st.extra["C"], OH=oh_, OW=ow_, K=st.extra["K"], S=st.extra["S"],
+                         pad=(st.extra["K"] - 1) // 2, Cs=st.extra["Cs"])
+                if st.kind == "dwk":
+                    nt = C.dwk_tiles(g)[3]
+                else:
+                    nt = C.mbconv_ed_tiles(dict(g, ldx=st.extra["ldx"], cin=st.extra["cin"]))[2]
                 self.ntiles[st.extra["blk"]] = nt
                 mx = max(mx, nt * st.extra["Cs"])
         self.pool_per_image = mx
@@ -194,6 +216,17 @@ class EfficientNetEngine(EngineBase):
                                          y=self._ptr("D"), pool=self._ptr("pool"), w1=_lib.ptr(w1),
                                          Cs=step.extra["Cs"], B=b, H=H, W=W, C=step.extra["C"], OH=OH, OW=OW,
                                          K=K, S=step.extra["S"], pad=(K - 1) // 2, act=2))
+        elif step.kind == "mbed":
+            w, bias = self.dw[step.extra["blk"]]
+            w1 = self.se[step.extra["blk"]][0]
+            lay = self.expand[step.extra["blk"]]
+            K = step.extra["K"]
+            prog.add_mbconv_ed(step.name, dict(x=self._ptr(step.src), we=_lib.ptr(lay.wp), be=_lib.ptr(lay.bias),
+                                               wd=_lib.ptr(w), bd=_lib.ptr(bias), y=self._ptr("D"),
+                                               pool=self._ptr("pool"), w1=_lib.ptr(w1), B=b, H=H, W=W,
+                                               ldx=step.extra["ldx"], cin=step.extra["cin"], C=step.extra["C"],
+                                               OH=OH, OW=OW, K=K, S=step.extra["S"], pad=(K - 1) // 2,
+                                               Cs=step.extra["Cs"]))
         elif step.kind == "se":
             _, b1, w2t, b2 = self.se[step.extra["blk"]]
             prog.add_se(step.name, dict(pool=self._ptr("pool"), b1=_lib.ptr(b1),
