@@ -134,7 +134,7 @@ MbedArgs mb_args(const py::dict& d) {
   MbedArgs a{};
   a.x = P<const uint16_t>(d, "x"); a.we = P<const uint16_t>(d, "we"); a.be = P<const float>(d, "be");
   a.wd = P<const float>(d, "wd"); a.bd = P<const float>(d, "bd"); a.y = P<uint16_t>(d, "y");
-  a.pool = P<float>(d, "pool"); a.w1 = P<const float>(d, "w1");
+  a.pool = P<float>(d, "pool"); a.w1 = P<const float>(d, "w1"); a.blob = P<const void>(d, "blob");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.ldx = I(d, "ldx"); a.cin = I(d, "cin");
   a.C = I(d, "C"); a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.K = I(d, "K"); a.S = I(d, "S");
   a.pad = I(d, "pad"); a.Cs = I(d, "Cs"); a.abl = I(d, "abl");
@@ -303,6 +303,7 @@ PYBIND11_MODULE(_C, m) {
     mbconv_ed_tiles(a, &rb, &tw, &nt);
     return py::make_tuple(rb, tw, nt);
   });
+  m.def("mbconv_blob_bytes", [](int cin, int K, int Cs) { return mbconv_blob_bytes(cin, K, Cs); });
   m.def("weight_scale", [](py::dict d, uintptr_t s) {
     const auto a = ws_args(d);
     py::gil_scoped_release nogil;

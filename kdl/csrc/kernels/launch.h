@@ -220,11 +220,13 @@ struct MbedArgs {
   uint16_t* y;            // [B][OH][OW][C] depthwise output
   float* pool;            // [B][ntiles][Cs] fc1 partials
   const float* w1;        // [Cs][C]
+  const void* blob;       // per-channel-block parameter blobs [C/32][mbconv_blob_bytes] (mbconv.hip)
   int B, H, W, ldx, cin, C, OH, OW, K, S, pad, Cs;
   int abl;                // timing ablations (tools only): 1 no depthwise, 2 no expand MFMA, 4 no reductions
 };
 hipError_t mbconv_ed(const MbedArgs& a, hipStream_t s);
 void mbconv_ed_tiles(const MbedArgs& a, int* rb, int* tw, int* ntiles);
+int mbconv_blob_bytes(int cin, int K, int Cs);
 
 // Squeeze-excite tail: scale[b][c] = sigmoid(W2 SiLU(sum_parts pool / HW + b1) + b2).
 struct SeArgs {

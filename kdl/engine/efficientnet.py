@@ -44,6 +44,28 @@ def _fold(p, conv, bn):
     return w, s, t
 
 
+def mbconv_blobs(lay: ConvGemmLayer, dw: tuple, w1: torch.Tensor, K: int, nbytes: int) -> torch.Tensor:
+    """Per-32-channel-block parameter blobs of the fused MBConv kernel (layout: mbconv.hip):
+    expand B fragments (2cb + j, t) | depthwise weights [K*K][32] | biases expand[32],
+    depthwise[32] | fc1 slice [Cs][32], fp32 except the bf16 fragments, each blob padded to
+    ``nbytes``. One contiguous read per block instead of four scattered ones."""
+    wd, bd = dw
+    KT = lay.K // 32
+    C = wd.shape[1]
+    frags = lay.wp.view(-1, KT, 512)                     # [nf][KT][64 lanes x 8] bf16
+    out = torch.zeros(C // 32, nbytes, dtype=torch.uint8, device=wd.device)
+    for cb in range(C // 32):
+        sl = slice(cb * 32, cb * 32 + 32)
+        parts = [frags[2 * cb:2 * cb + 2].reshape(-1).view(torch.uint8),
+                 wd[:, sl].contiguous().view(torch.uint8).reshape(-1),
+                 lay.bias[sl].contiguous().view(torch.uint8), bd[sl].contiguous().view(torch.uint8),
+                 w1[:, sl].contiguous().view(torch.uint8).reshape(-1)]
+        blob = torch.cat(parts)
+        assert blob.numel() <= nbytes, (blob.numel(), nbytes)
+        out[cb, :blob.numel()] = blob
+    return out.contiguous()
+
+
 class EfficientNetEngine(EngineBase):
     model_name = "efficientnet_b7"
 
@@ -84,7 +106,7 @@ class EfficientNetEngine(EngineBase):
         self.steps.append(Step("stem", "stem", src="input", dst="X0", geom=(self.size, self.size, H, H)))
         self._need("X0", H * H * E.STEM)
         cur, ldc, ping = "X0", E.STEM, 0
-        self.dw, self.se, self.expand = {}, {}, {}
+        self.dw, self.se, self.expand, self.blobs = {}, {}, {}, {}
         C = _lib.lib()
         for blk in E.blocks():
             n = blk.names()
@@ -107,6 +129,8 @@ class EfficientNetEngine(EngineBase):
                 fused = self.mbed and C.mbconv_ed_tiles(dict(geo, cin=lay.cin_pad))[2] > 0
                 if fused:
                     self.expand[blk.prefix] = lay
+                    self.blobs[blk.prefix] = mbconv_blobs(lay, self.dw[blk.prefix], self.se[blk.prefix][0], blk.k,
+                                                          C.mbconv_blob_bytes(lay.cin_pad, blk.k, blk.csq))
                     self.steps.append(Step("mbed", f"{blk.prefix}.mbed", src=cur, dst="D", geom=(H, H, oh, oh),
                                            extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix,
                                                       ldx=ldc, cin=lay.cin_pad)))
@@ -221,7 +245,8 @@ class EfficientNetEngine(EngineBase):
             w1 = self.se[step.extra["blk"]][0]
             lay = self.expand[step.extra["blk"]]
             K = step.extra["K"]
-            prog.add_mbconv_ed(step.name, dict(x=self._ptr(step.src), we=_lib.ptr(lay.wp), be=_lib.ptr(lay.bias),
+            prog.add_mbconv_ed(step.name, dict(x=self._ptr(step.src), blob=_lib.ptr(self.blobs[step.extra["blk"]]),
+                                               we=_lib.ptr(lay.wp), be=_lib.ptr(lay.bias),
                                                wd=_lib.ptr(w), bd=_lib.ptr(bias), y=self._ptr("D"),
                                                pool=self._ptr("pool"), w1=_lib.ptr(w1), B=b, H=H, W=W,
                                                ldx=step.extra["ldx"], cin=step.extra["cin"], C=step.extra["C"],

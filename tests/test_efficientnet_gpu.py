@@ -83,7 +83,9 @@ def test_mbconv_fused_expand_depthwise_matches_unfused(cin, C, K, S, H):
     C_.dwk(dict(geo, x=e.data_ptr(), w=wk.data_ptr(), bias=bd.data_ptr(), y=y0.data_ptr(),
                 pool=pool0.data_ptr(), w1=w1.data_ptr(), act=2), s)
     # fused
-    mg = dict(geo, ldx=cin, cin=cin)
+    from kdl.engine.efficientnet import mbconv_blobs
+    blob = mbconv_blobs(lay, (wk, bd), w1, K, C_.mbconv_blob_bytes(cin, K, Cs))
+    mg = dict(geo, ldx=cin, cin=cin, blob=blob.data_ptr())
     rb, tw, nt = C_.mbconv_ed_tiles(mg)
     assert nt > 0, (rb, tw)
     y1 = torch.full((B, OH, OH, C), float("nan"), dtype=torch.bfloat16, device=DEV)

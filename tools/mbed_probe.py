@@ -29,7 +29,9 @@ def main():
         bd = torch.zeros(C).cuda()
         w1 = (torch.randn(Cs, C) / C ** 0.5).cuda()
         y = torch.zeros(B * OH * OH * C, dtype=torch.bfloat16, device="cuda")
-        mg = dict(B=B, H=H, W=H, C=C, OH=OH, OW=OH, K=K, S=S, pad=pad, Cs=Cs, ldx=cin, cin=cin)
+        from kdl.engine.efficientnet import mbconv_blobs
+        blob = mbconv_blobs(lay, (wk, bd), w1, K, C_.mbconv_blob_bytes(cin, K, Cs))
+        mg = dict(B=B, H=H, W=H, C=C, OH=OH, OW=OH, K=K, S=S, pad=pad, Cs=Cs, ldx=cin, cin=cin, blob=blob.data_ptr())
         rb, tw, nt = C_.mbconv_ed_tiles(mg)
         pool = torch.zeros(B * nt * Cs, device="cuda")
         e = torch.zeros(B * H * H * C, dtype=torch.bfloat16, device="cuda")
