@@ -121,8 +121,9 @@ PYBIND11_MODULE(_rt, m) {
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
       .def(py::init([](int max_batch_size, int64_t batch_timeout_us, int max_enqueued_batches,
-                       std::vector<int> allowed_batch_sizes, size_t item_bytes, int out_cols) {
+                       std::vector<int> allowed_batch_sizes, size_t item_bytes, int out_cols, int copy_threads) {
              BatcherOptions o;
+             o.copy_threads = copy_threads;
              o.max_batch_size = max_batch_size;
              o.batch_timeout_us = batch_timeout_us;
              o.max_enqueued_batches = max_enqueued_batches;
@@ -133,7 +134,7 @@ PYBIND11_MODULE(_rt, m) {
            }),
            py::arg("max_batch_size") = 32, py::arg("batch_timeout_us") = 2000,
            py::arg("max_enqueued_batches") = 1000, py::arg("allowed_batch_sizes") = std::vector<int>{},
-           py::arg("item_bytes") = 0, py::arg("out_cols") = 0)
+           py::arg("item_bytes") = 0, py::arg("out_cols") = 0, py::arg("copy_threads") = 4)
       // `data` must stay alive until wait() returns (the Python wrapper holds it).
       .def("submit", [](DynamicBatcher& b, py::buffer data, int n_items, int64_t deadline_us) {
         py::buffer_info info = data.request();

@@ -32,6 +32,7 @@ struct BatcherOptions {
   std::vector<int> allowed_batch_sizes;      // sorted ascending; empty = exact batch sizes
   size_t item_bytes = 0;
   int out_cols = 0;                          // floats per item result row
+  int copy_threads = 4;                      // threads for a batch's payload copy into staging
 };
 
 enum BatchStatus { ST_OK = 0, ST_DEADLINE = 1, ST_SHUTDOWN = 2, ST_ERROR = 3, ST_PENDING = 4, ST_QUEUE_FULL = 5 };

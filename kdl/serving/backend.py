@@ -427,7 +427,9 @@ class SignatureRunner:
         self.batcher = _lib.rt().DynamicBatcher(max_batch_size=self.max_batch, batch_timeout_us=timeout,
                                                 max_enqueued_batches=bp.max_enqueued_batches,
                                                 allowed_batch_sizes=self.buckets, item_bytes=item_bytes,
-                                                out_cols=source.classes)
+                                                out_cols=source.classes,
+                                                # threads for a batch's payload copy into pinned staging
+                                                copy_threads=int(os.environ.get("KDL_COPY_THREADS", "4")))
         self.executors: list[_Executor] = []
         self.faults = FaultInjector()
         if devices:

@@ -123,3 +123,23 @@ def test_many_concurrent_clients_two_consumers():
         c.join()
     assert not errors
     assert b.stats()["completed"] == 200
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_large_payloads_copied_in_parallel_pieces(threads):
+    """Batches of several MB are copied into staging in 1 MiB pieces by up to copy_threads
+    threads: every byte must land at its request's item offset (299x299x3 items)."""
+    item = 299 * 299 * 3
+    b = rt.DynamicBatcher(max_batch_size=8, batch_timeout_us=1_000_000, max_enqueued_batches=10,
+                          allowed_batch_sizes=[8], item_bytes=item, out_cols=1, copy_threads=threads)
+    rng = np.random.default_rng(threads)
+    reqs = [rng.integers(0, 256, n * item, dtype=np.uint8) for n in (3, 1, 4)]
+    tickets = [b.submit(r, len(r) // item, 0) for r in reqs]
+    staging = np.zeros(8 * item, np.uint8)
+    batch = b.next_batch(staging.ctypes.data, 1_000_000)
+    assert batch is not None and batch.n_real == 8
+    assert np.array_equal(staging, np.concatenate(reqs))
+    out = np.zeros((8, 1), np.float32)
+    b.finish(batch, out.ctypes.data, rt.ST_OK)
+    for t, r in zip(tickets, reqs):
+        assert b.wait(t, np.zeros((len(r) // item, 1), np.float32)) == rt.ST_OK
