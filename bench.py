@@ -75,6 +75,12 @@ def main(argv=None) -> int:
     ap.add_argument("--profile-layers", action="store_true")
     ap.add_argument("--save-tuning", default=None, help="write the autotune result (rank 0) to this path")
     ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # gloo: pipeline logic checks
+    ap.add_argument("--egress", choices=["gather", "local"], default="gather",
+                    help="gather: RCCL-gather every step's logits to rank 0 (+ D2H there); local: each rank "
+                         "D2Hs its own logits (what per-GPU serving executors do)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the multi-rank code path (process group, RCCL gather) even with one rank: "
+                         "measures the collective overhead on a 1-GPU box")
     a = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,7 +91,8 @@ def main(argv=None) -> int:
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    dist_on = world > 1 or a.force_dist
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -146,7 +153,8 @@ def main(argv=None) -> int:
     # i+depth lands in one slot (H2D, or RCCL scatter) and batch i-1's logits leave
     # another while batch i's graph runs; no device-to-device copies anywhere.
     slots = eng.add_input_slots(NS)
-    direct = world == 1 or a.ingress != "scatter"    # H2D straight into the slot
+    direct = not dist_on or a.ingress != "scatter"    # H2D straight into the slot
+    gather = dist_on and a.egress == "gather"
     stage = ([torch.empty((n_host, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(NS)]
              if has_host and not direct else [None] * NS)
     NC = info.classes
@@ -155,10 +163,10 @@ def main(argv=None) -> int:
     out_host = [torch.zeros((n_global, NC), dtype=torch.float32).pin_memory() for _ in range(NS)]
     s = eng.stream                          # compute: graph replays
     cs = torch.cuda.Stream(device=dev)      # ingress H2D
-    ms = torch.cuda.Stream(device=dev) if world > 1 else None   # RCCL scatter / gather + egress D2H
+    ms = torch.cuda.Stream(device=dev) if gather or not direct else None   # RCCL scatter / gather + egress D2H
     # egress D2H (one GPU); stage-pipelined engines copy out on their last stage's stream
     # instead, so compute stages + H2D + egress stay within GPU_MAX_HW_QUEUES (4)
-    ds = torch.cuda.Stream(device=dev) if world == 1 and not a.stages else None
+    ds = torch.cuda.Stream(device=dev) if not gather and not a.stages else None
     E = lambda: [torch.cuda.Event() for _ in range(NS)]  # noqa: E731
     ready, scattered, drained = E(), E(), E()
     # free[j]: slot j's input and logits are final -- one event per lane (free-running
@@ -218,7 +226,7 @@ def main(argv=None) -> int:
     def collect(i, timed=False):
         j = i % NS
         out = eng.slot_logits(j)[:B]
-        if world > 1:
+        if gather:
             # gather + D2H on the comm stream: one fewer stream, so compute, lanes, H2D
             # and comm each keep a hardware queue of their own (GPU_MAX_HW_QUEUES=4)
             with torch.cuda.stream(ms):
@@ -271,14 +279,14 @@ def main(argv=None) -> int:
         for _ in range(10):
             eng.launch(B, s, capture=use_graph)
         torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     for i in range(a.depth):
         ingress(i)
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
 
@@ -288,18 +296,18 @@ def main(argv=None) -> int:
         step(i)
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     # unloaded per-batch latency (same path, one batch in flight at a time), outside the timed region
     lat = []
     for k in range(min(20, total)):
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
         ingress(k, timed=True)
@@ -307,7 +315,7 @@ def main(argv=None) -> int:
         collect(k, timed=True)
         torch.cuda.synchronize()
         lat.append(t_in[k].elapsed_time(t_out[k]))
-    if world > 1:
+    if dist_on:
         t = torch.tensor(lat, device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         lat = t.tolist()
@@ -339,7 +347,7 @@ def main(argv=None) -> int:
             "config": {"model": info.description,
                        "global_batch": n_global, "seq_len": None, "image_size": S,
                        "per_gpu_batch": B, "parallelism": f"dp{world}",
-                       "ingress": a.ingress, "hipgraph": use_graph, "lanes": a.lanes,
+                       "ingress": a.ingress, "egress": a.egress if dist_on else "local", "hipgraph": use_graph, "lanes": a.lanes,
                        **({"stages": f"{len(eng.ranges)} (cut after {a.stages})"} if a.stages else {})},
         }
         print(json.dumps(res), flush=True)
@@ -348,7 +356,7 @@ def main(argv=None) -> int:
         if a.profile_layers:
             for name, t in eng.profile(B, 10):
                 print(f"{name:28s} {t * 1e3:9.1f} us", file=sys.stderr)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     return 0
 
