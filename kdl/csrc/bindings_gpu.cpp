@@ -115,6 +115,8 @@ DwkArgs dwk_args(const py::dict& d) {
   a.y = P<uint16_t>(d, "y"); a.pool = P<float>(d, "pool"); a.w1 = P<const float>(d, "w1");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.C = I(d, "C"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
   a.K = I(d, "K"); a.S = I(d, "S", 1); a.pad = I(d, "pad"); a.act = I(d, "act"); a.Cs = I(d, "Cs");
+  a.cg = I(d, "cg", 0); a.rb = I(d, "rb", 0); a.tw = I(d, "tw", 0); a.seg = I(d, "seg", 0);
+  a.lds_kb = I(d, "lds_kb", 0);
   return a;
 }
 SeArgs se_args(const py::dict& d) {
@@ -280,7 +282,7 @@ PYBIND11_MODULE(_C, m) {
     const auto a = dwk_args(d);
     int cg, rb, tw, nt;
     dwk_tiles(a, &cg, &rb, &tw, &nt);
-    return py::make_tuple(cg, rb, tw, nt);
+    return py::make_tuple(cg, rb, tw, nt, dwk_seg(a));
   });
   m.def("squeeze_excite", [](py::dict d, uintptr_t s) {
     const auto a = se_args(d);

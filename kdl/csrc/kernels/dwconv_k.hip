@@ -52,6 +52,12 @@ __global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int
   int c = tid % CG, t = tid / CG;
   int col = t % PC, r = t / PC;
   const long img = (long)b * a.H;
+  // stride 2: the patch is stored column-deinterleaved (even columns, then odd), so the
+  // items of a wave -- SEG*S columns apart -- start on different 16-byte bank slots when
+  // SEG is odd (ds_read_b128 conflicts within 16-lane groups otherwise: an even distance
+  // puts every item of a chunk on the same slot)
+  const int PCe = (PC + 1) >> 1;
+  auto pcol = [&](int cc) { return S == 2 ? (cc & 1) * PCe + (cc >> 1) : cc; };
   for (int base = 0; base < nst; base += 256 * DWK_MAXL) {
     u32x4 v[DWK_MAXL];
     int cc[DWK_MAXL], cl[DWK_MAXL], rr[DWK_MAXL];
@@ -72,7 +78,7 @@ __global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int
     }
 #pragma unroll
     for (int l = 0; l < DWK_MAXL; ++l)
-      if (base + tid + l * 256 < nst) *(u32x4*)(xsm + (((long)rr[l] * PC + cl[l]) * CG + cc[l]) * 16) = v[l];
+      if (base + tid + l * 256 < nst) *(u32x4*)(xsm + (((long)rr[l] * PC + pcol(cl[l])) * CG + cc[l]) * 16) = v[l];
   }
   __syncthreads();
 
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int
 #pragma unroll
       for (int j = 0; j < (SEG - 1) * S + K; ++j) {
         const int lc = min(w0 * S + j, PC - 1);   // clamping only feeds outputs that are not stored
-        const u32x4 v = *(const u32x4*)(rowp + (long)lc * CG * 16);
+        const u32x4 v = *(const u32x4*)(rowp + (long)pcol(lc) * CG * 16);
         f32x2 xv[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) xv[d] = (f32x2){bf_lo(v[d]), bf_hi(v[d])};
@@ -188,37 +194,82 @@ static size_t dwk_smem(int K, int S, int CG, int RB, int TW) {
   return w + patch > red ? w + patch : red;
 }
 
-// Tile choice: column tiles of <= 48 outputs; for each power-of-two chunk group
-// CG dividing C/8 the tallest row band that fits 96 KiB of LDS; keep the CG with
-// the tallest band (halo re-reads (RB-1)S+K over RB*S rows), ties -> wider CG.
+// Tile choice. Measured (tools/dwkbench.py --grid, batch 32, profiles/dwk_sweep.txt): the
+// EfficientNet-B7 shapes take their best (cg, rb, tw, seg) from the table below; any other
+// shape gets the fallback: column tiles of <= 38 outputs (19 at stride 2), for each
+// power-of-two chunk group CG in {8, 4, 2, 1} dividing C/8 the tallest row band (<= 8) that
+// fits 52 KiB of LDS -- three workgroups per CU, so one tile's staging loads overlap the
+// others' arithmetic (the first heuristic filled 96 KiB: one workgroup, one wave per SIMD,
+// 25 % slower summed over B7) -- keep the CG with the tallest band, ties -> wider CG.
+// SEG odd: the items of a wave then start on different LDS bank slots (stride 2: with the
+// patch column-deinterleaved). a.cg/rb/tw/seg override everything.
+struct DwkTile { short H, W, C, K, S, cg, rb, tw, seg; };
+static const DwkTile kDwkTable[] = {
+    {300, 300, 64, 3, 1, 8, 8, 38, 5},   {300, 300, 32, 3, 1, 4, 16, 43, 4},  {300, 300, 192, 3, 2, 4, 6, 30, 3},
+    {150, 150, 288, 3, 1, 4, 12, 50, 5}, {150, 150, 288, 5, 2, 4, 8, 19, 3},  {75, 75, 480, 5, 1, 4, 8, 38, 5},
+    {75, 75, 480, 3, 2, 4, 8, 19, 3},    {38, 38, 960, 3, 1, 8, 8, 19, 5},    {38, 38, 960, 5, 1, 4, 8, 38, 5},
+    {38, 38, 1344, 5, 1, 4, 8, 38, 5},   {38, 38, 1344, 5, 2, 4, 8, 19, 3},   {19, 19, 2304, 5, 1, 8, 12, 19, 5},
+    {19, 19, 2304, 3, 1, 8, 8, 19, 5},   {19, 19, 3840, 3, 1, 8, 12, 19, 5},
+};
+
+static const DwkTile* dwk_lookup(const DwkArgs& a) {
+  for (const DwkTile& t : kDwkTable)
+    if (t.H == a.H && t.W == a.W && t.C == a.C && t.K == a.K && t.S == a.S) return &t;
+  return nullptr;
+}
+
 void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles) {
   const int C8 = a.C / 8;
-  const int ncol = (a.OW + 47) / 48;
-  const int TW = (a.OW + ncol - 1) / ncol;
-  int bestcg = 1, bestrb = 0;
-  for (int CG : {8, 4, 2, 1}) {
-    if (C8 % CG != 0) continue;
-    int RB = 1;
-    while (RB < a.OH && RB < 16 && dwk_smem(a.K, a.S, CG, RB + 1, TW) <= 96 * 1024) ++RB;
-    if (dwk_smem(a.K, a.S, CG, RB, TW) > 96 * 1024) continue;
-    if (RB > bestrb) { bestrb = RB; bestcg = CG; }
+  const DwkTile* t = dwk_lookup(a);
+  if (a.cg > 0 && a.rb > 0 && a.tw > 0) {
+    *cg = a.cg; *rb = a.rb; *tw = a.tw;
+  } else if (t != nullptr && a.lds_kb == 0) {
+    *cg = t->cg; *rb = t->rb; *tw = t->tw;
+  } else {
+    const int budget = (a.lds_kb > 0 ? a.lds_kb : 52) * 1024;
+    const int cap = a.S == 1 ? 38 : 19;
+    const int ncol = (a.OW + cap - 1) / cap;
+    const int TW = (a.OW + ncol - 1) / ncol;
+    int bestcg = 1, bestrb = 0;
+    for (int CG : {8, 4, 2, 1}) {
+      if (C8 % CG != 0) continue;
+      int RB = 1;
+      while (RB < a.OH && RB < 8 && dwk_smem(a.K, a.S, CG, RB + 1, TW) <= (size_t)budget) ++RB;
+      if (dwk_smem(a.K, a.S, CG, RB, TW) > (size_t)budget) continue;
+      if (RB > bestrb) { bestrb = RB; bestcg = CG; }
+    }
+    if (bestrb == 0) bestrb = 1;
+    *cg = bestcg; *rb = bestrb; *tw = TW;
   }
-  if (bestrb == 0) bestrb = 1;
-  *cg = bestcg; *rb = bestrb; *tw = TW;
-  *ntiles = ((a.OH + bestrb - 1) / bestrb) * ((a.OW + TW - 1) / TW) * ((a.C / 8) / bestcg);
+  *ntiles = ((a.OH + *rb - 1) / *rb) * ((a.OW + *tw - 1) / *tw) * (C8 / *cg);
+}
+
+int dwk_seg(const DwkArgs& a) {
+  if (a.seg > 0) return a.seg;
+  const DwkTile* t = dwk_lookup(a);
+  if (t != nullptr && a.lds_kb == 0 && a.cg == 0) return t->seg;
+  return a.S == 1 ? 5 : 3;
 }
 
 hipError_t dwk(const DwkArgs& a, hipStream_t s) {
   if (a.C % 8 != 0 || a.B <= 0 || (a.K != 3 && a.K != 5) || (a.S != 1 && a.S != 2)) return hipErrorInvalidValue;
   int CG, RB, TW, nt;
   dwk_tiles(a, &CG, &RB, &TW, &nt);
+  // CG: a power of two <= 8 dividing C/8 (fixed chunk per thread; the pool reduction's
+  // CG*8 channel sums fit the 64-float tail of the reduction buffer)
+  if ((CG & (CG - 1)) != 0 || CG > 8 || (a.C / 8) % CG != 0 || RB <= 0 || TW <= 0) return hipErrorInvalidValue;
   const size_t smem = dwk_smem(a.K, a.S, CG, RB, TW);
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   const long nblk = (long)a.B * nt;          // nt counts (row band, column tile, channel group)
+  if (nblk >= (1L << 31)) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk), block(256);
-#define KDL_DWK(k, st) \
-  if (a.K == k && a.S == st) { hipLaunchKernelGGL((dwk_kernel<k, st, 4>), grid, block, smem, s, a, CG, RB, TW); return hipGetLastError(); }
-  KDL_DWK(3, 1) KDL_DWK(3, 2) KDL_DWK(5, 1) KDL_DWK(5, 2)
+  const int seg = dwk_seg(a);
+#define KDL_DWK(k, st, sg) \
+  if (a.K == k && a.S == st && seg == sg) { \
+    hipLaunchKernelGGL((dwk_kernel<k, st, sg>), grid, block, smem, s, a, CG, RB, TW); return hipGetLastError(); }
+#define KDL_DWK_SEGS(k, st) KDL_DWK(k, st, 3) KDL_DWK(k, st, 4) KDL_DWK(k, st, 5) KDL_DWK(k, st, 7) KDL_DWK(k, st, 8)
+  KDL_DWK_SEGS(3, 1) KDL_DWK_SEGS(3, 2) KDL_DWK_SEGS(5, 1) KDL_DWK_SEGS(5, 2)
+#undef KDL_DWK_SEGS
 #undef KDL_DWK
   return hipErrorInvalidValue;
 }

@@ -205,9 +205,12 @@ struct DwkArgs {
   const float* w1;        // SE fc1 [Cs][C]
   int B, H, W, C, OH, OW, K, S, pad, act;   // act: 0 none, 2 SiLU
   int Cs;
+  int cg, rb, tw, seg;    // tile override (0: host heuristic; tools/dwkbench.py sweeps these)
+  int lds_kb;             // heuristic's LDS budget per workgroup (0: default)
 };
 hipError_t dwk(const DwkArgs& a, hipStream_t s);
 void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles);
+int dwk_seg(const DwkArgs& a);
 
 // Fused MBConv front half (mbconv.hip): expand 1x1 + BN + SiLU -> KxK/S depthwise + BN + SiLU
 // -> SE pool / fc1 partials, the expanded tensor staying in LDS.

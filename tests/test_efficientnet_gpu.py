@@ -16,9 +16,16 @@ def _rel(a, b):
     return ((a.float().cpu() - b.float().cpu()).abs().max() / b.float().abs().max()).item()
 
 
-@pytest.mark.parametrize("K,S,H,C", [(3, 1, 37, 64), (3, 2, 75, 288), (5, 1, 19, 1344), (5, 2, 150, 192),
-                                     (5, 2, 38, 960)])
-def test_dwk_silu_and_fused_squeeze_excite(K, S, H, C):
+@pytest.mark.parametrize("K,S,H,C,tile", [
+    (3, 1, 37, 64, None), (3, 2, 75, 288, None), (5, 1, 19, 1344, None), (5, 2, 150, 192, None),
+    (5, 2, 38, 960, None),
+    # measured-table shapes (kDwkTable) and explicit tiles: odd / even SEG, ragged column and
+    # row tiles, stride-2 column-deinterleaved patches, every CG
+    (5, 2, 38, 1344, None), (3, 1, 19, 2304, None),
+    (3, 2, 75, 480, dict(cg=4, rb=8, tw=19, seg=3)), (5, 2, 38, 960, dict(cg=8, rb=3, tw=7, seg=7)),
+    (5, 1, 38, 960, dict(cg=2, rb=5, tw=13, seg=8)), (3, 1, 37, 64, dict(cg=1, rb=16, tw=37, seg=4)),
+    (3, 2, 37, 64, dict(cg=8, rb=1, tw=5, seg=5))])
+def test_dwk_silu_and_fused_squeeze_excite(K, S, H, C, tile):
     gen = torch.Generator().manual_seed(K * 100 + S * 10 + H)
     B, Cs = 2, max(1, C // 24)
     pad = (K - 1) // 2
@@ -31,7 +38,7 @@ def test_dwk_silu_and_fused_squeeze_excite(K, S, H, C):
     wk = w[:, 0].permute(1, 2, 0).reshape(K * K, C).contiguous()
     y = torch.zeros(B, OH, OH, C, dtype=torch.bfloat16, device=DEV)
     C_ = _lib.lib()
-    args = dict(B=B, H=H, W=H, C=C, OH=OH, OW=OH, K=K, S=S, pad=pad, Cs=Cs)
+    args = dict(B=B, H=H, W=H, C=C, OH=OH, OW=OH, K=K, S=S, pad=pad, Cs=Cs, **(tile or {}))
     nt = C_.dwk_tiles(args)[3]
     pool = torch.zeros(B, nt, Cs, device=DEV)
     scale = torch.zeros(B, C, device=DEV)
