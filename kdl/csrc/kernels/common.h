@@ -20,6 +20,9 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// SiLU with a hardware reciprocal: v_exp + v_rcp + v_mul instead of the IEEE division
+// sequence (~10 VALU ops) -- the depthwise kernels evaluate it per output element
+__device__ __forceinline__ float fast_silu(float v) { return v * __builtin_amdgcn_rcpf(1.f + __expf(-v)); }
 __device__ __forceinline__ float bf_lo(uint32_t d) { return __uint_as_float(d << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t d) { return __uint_as_float(d & 0xffff0000u); }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }

@@ -10,6 +10,8 @@
 // an item = (chunk, row, SEG-column segment) slides a register window along W.
 // SE partial sums are reduced in a fixed order (deterministic, no atomics):
 // CG divides 256, so every item of a thread has the same chunk.
+#include <cstdlib>
+
 #include "common.h"
 #include "launch.h"
 
@@ -17,7 +19,7 @@ namespace kdl {
 
 constexpr int DWK_MAXL = 8;
 
-__device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
+__device__ __forceinline__ float silu(float v) { return fast_silu(v); }
 
 template <int K, int S, int SEG>
 __global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int TW) {
@@ -203,13 +205,13 @@ static size_t dwk_smem(int K, int S, int CG, int RB, int TW) {
 // 25 % slower summed over B7) -- keep the CG with the tallest band, ties -> wider CG.
 // SEG odd: the items of a wave then start on different LDS bank slots (stride 2: with the
 // patch column-deinterleaved). a.cg/rb/tw/seg override everything.
-struct DwkTile { short H, W, C, K, S, cg, rb, tw, seg; };
+struct DwkTile { short H, W, C, K, S, algo, cg, rb, tw, seg; };   // algo 2: rb / seg of dwv_kernel
 static const DwkTile kDwkTable[] = {
-    {300, 300, 64, 3, 1, 8, 8, 38, 5},   {300, 300, 32, 3, 1, 4, 16, 43, 4},  {300, 300, 192, 3, 2, 4, 6, 30, 3},
-    {150, 150, 288, 3, 1, 4, 12, 50, 5}, {150, 150, 288, 5, 2, 4, 8, 19, 3},  {75, 75, 480, 5, 1, 4, 8, 38, 5},
-    {75, 75, 480, 3, 2, 4, 8, 19, 3},    {38, 38, 960, 3, 1, 8, 8, 19, 5},    {38, 38, 960, 5, 1, 4, 8, 38, 5},
-    {38, 38, 1344, 5, 1, 4, 8, 38, 5},   {38, 38, 1344, 5, 2, 4, 8, 19, 3},   {19, 19, 2304, 5, 1, 8, 12, 19, 5},
-    {19, 19, 2304, 3, 1, 8, 8, 19, 5},   {19, 19, 3840, 3, 1, 8, 12, 19, 5},
+    {300, 300, 64, 3, 1, 2, 0, 16, 0, 4},   {300, 300, 32, 3, 1, 2, 0, 16, 0, 2},  {300, 300, 192, 3, 2, 2, 0, 6, 0, 2},
+    {150, 150, 288, 3, 1, 2, 0, 38, 0, 2},  {150, 150, 288, 5, 2, 2, 0, 16, 0, 4}, {75, 75, 480, 5, 1, 1, 4, 8, 38, 5},
+    {75, 75, 480, 3, 2, 2, 0, 38, 0, 2},    {38, 38, 960, 3, 1, 2, 0, 8, 0, 4},    {38, 38, 960, 5, 1, 1, 4, 8, 38, 5},
+    {38, 38, 1344, 5, 1, 1, 4, 8, 38, 5},   {38, 38, 1344, 5, 2, 2, 0, 12, 0, 2},  {19, 19, 2304, 5, 1, 1, 8, 12, 19, 5},
+    {19, 19, 2304, 3, 1, 1, 8, 8, 19, 5},   {19, 19, 3840, 3, 1, 1, 8, 12, 19, 5},
 };
 
 static const DwkTile* dwk_lookup(const DwkArgs& a) {
@@ -218,12 +220,12 @@ static const DwkTile* dwk_lookup(const DwkArgs& a) {
   return nullptr;
 }
 
-void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles) {
+static void dwt_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles) {
   const int C8 = a.C / 8;
   const DwkTile* t = dwk_lookup(a);
   if (a.cg > 0 && a.rb > 0 && a.tw > 0) {
     *cg = a.cg; *rb = a.rb; *tw = a.tw;
-  } else if (t != nullptr && a.lds_kb == 0) {
+  } else if (t != nullptr && t->algo == 1 && a.lds_kb == 0) {
     *cg = t->cg; *rb = t->rb; *tw = t->tw;
   } else {
     const int budget = (a.lds_kb > 0 ? a.lds_kb : 52) * 1024;
@@ -244,17 +246,16 @@ void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles) {
   *ntiles = ((a.OH + *rb - 1) / *rb) * ((a.OW + *tw - 1) / *tw) * (C8 / *cg);
 }
 
-int dwk_seg(const DwkArgs& a) {
+static int dwt_seg(const DwkArgs& a) {
   if (a.seg > 0) return a.seg;
   const DwkTile* t = dwk_lookup(a);
-  if (t != nullptr && a.lds_kb == 0 && a.cg == 0) return t->seg;
+  if (t != nullptr && t->algo == 1 && a.lds_kb == 0 && a.cg == 0) return t->seg;
   return a.S == 1 ? 5 : 3;
 }
 
-hipError_t dwk(const DwkArgs& a, hipStream_t s) {
-  if (a.C % 8 != 0 || a.B <= 0 || (a.K != 3 && a.K != 5) || (a.S != 1 && a.S != 2)) return hipErrorInvalidValue;
+static hipError_t dwt(const DwkArgs& a, hipStream_t s) {
   int CG, RB, TW, nt;
-  dwk_tiles(a, &CG, &RB, &TW, &nt);
+  dwt_tiles(a, &CG, &RB, &TW, &nt);
   // CG: a power of two <= 8 dividing C/8 (fixed chunk per thread; the pool reduction's
   // CG*8 channel sums fit the 64-float tail of the reduction buffer)
   if ((CG & (CG - 1)) != 0 || CG > 8 || (a.C / 8) % CG != 0 || RB <= 0 || TW <= 0) return hipErrorInvalidValue;
@@ -263,7 +264,7 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
   const long nblk = (long)a.B * nt;          // nt counts (row band, column tile, channel group)
   if (nblk >= (1L << 31)) return hipErrorInvalidValue;
   const dim3 grid((unsigned)nblk), block(256);
-  const int seg = dwk_seg(a);
+  const int seg = dwt_seg(a);
 #define KDL_DWK(k, st, sg) \
   if (a.K == k && a.S == st && seg == sg) { \
     hipLaunchKernelGGL((dwk_kernel<k, st, sg>), grid, block, smem, s, a, CG, RB, TW); return hipGetLastError(); }
@@ -271,6 +272,236 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
   KDL_DWK_SEGS(3, 1) KDL_DWK_SEGS(3, 2) KDL_DWK_SEGS(5, 1) KDL_DWK_SEGS(5, 2)
 #undef KDL_DWK_SEGS
 #undef KDL_DWK
+  return hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------- direct streaming variant
+// No LDS staging: a thread owns one 4-channel chunk (8-byte loads, 64 chunk lanes of a
+// wave read 512 contiguous bytes) and SEG adjacent output columns of a row band, and
+// streams the band's input rows top to bottom. Each input row is loaded once (the next
+// one is in flight while this one is used), unpacked once, and scattered into the
+// accumulators of the R = ceil(K/S) output rows it feeds; an output row is finished
+// (bias, SiLU, bf16 store, SE pool) when its last input row has passed. The row loop is
+// unrolled by R*S input rows so every accumulator slot index is a compile-time constant.
+// The tap weights live in registers for the whole band. What this replaces: the tiled
+// kernel above stages the whole patch, syncs, then computes, so one workgroup's loads never
+// overlap its own arithmetic and its LDS budget caps the CU at 1-3 workgroups.
+// Workgroup = CB chunk lanes x (256/CB) segment lanes of one (image, row band); the SE
+// partials are per workgroup (part = band x segment block x chunk block).
+template <int K, int S, int SEG, int CB>
+__global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
+  constexpr int R = (K + S - 1) / S;       // output rows in flight
+  constexpr int P = R * S;                 // unroll period (input rows)
+  constexpr int NJ = (SEG - 1) * S + K;    // input columns per thread
+  constexpr int SL = 256 / CB;             // segment lanes per workgroup
+  __shared__ float red[256 * 4 + CB * 4];
+  const int C4 = a.C >> 2;
+  const int nseg = (a.OW + SEG - 1) / SEG;
+  const int nsb = (nseg + SL - 1) / SL;
+  const int ncb = C4 / CB;
+  const int nbands = (a.OH + RB - 1) / RB;
+  int bid = blockIdx.x;
+  const int cbk = bid % ncb;
+  bid /= ncb;
+  const int sb = bid % nsb;
+  bid /= nsb;
+  const int band = bid % nbands;
+  const int b = bid / nbands;
+  const int tid = threadIdx.x;
+  const int cl = tid % CB, sl = tid / CB;
+  const int ch = (cbk * CB + cl) * 4;
+  const int seg = sb * SL + sl;
+  const bool live = seg < nseg;
+  const int w0 = seg * SEG;
+  const int h0 = band * RB;
+  const int rows = min(RB, a.OH - h0);
+  const int iw0 = w0 * S - a.pad, ih0 = h0 * S - a.pad;
+  const int vmax = (rows - 1) * S + K;
+
+  f32x2 wt[K * K][2];
+#pragma unroll
+  for (int t = 0; t < K * K; ++t) {
+    const float4 q = *(const float4*)(a.w + (long)t * a.C + ch);
+    wt[t][0] = (f32x2){q.x, q.y};
+    wt[t][1] = (f32x2){q.z, q.w};
+  }
+  const float4 bq = *(const float4*)(a.bias + ch);
+  f32x2 acc[R][SEG][2];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int o = 0; o < SEG; ++o) acc[r][o][0] = acc[r][o][1] = (f32x2){0.f, 0.f};
+  float psum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* xb = a.x + (long)b * a.H * a.W * a.C + ch;
+  uint16_t* yb = a.y + (long)b * a.OH * a.OW * a.C + ch;
+  bool cok[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cok[j] = live && (unsigned)(iw0 + j) < (unsigned)a.W;
+  auto load = [&](int v, u32x2 (&xr)[NJ]) {
+    const int ih = ih0 + v;
+    const bool rok = v < vmax && (unsigned)ih < (unsigned)a.H;
+    const uint16_t* rp = xb + ((long)ih * a.W + iw0) * a.C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      xr[j] = (rok && cok[j]) ? *(const u32x2*)(rp + (long)j * a.C) : (u32x2){0u, 0u};
+  };
+  auto finish = [&](f32x2 (&ac)[SEG][2], int ol) {
+    uint16_t* rp = yb + ((long)(h0 + ol) * a.OW + w0) * a.C;
+#pragma unroll
+    for (int o = 0; o < SEG; ++o) {
+      float f0 = ac[o][0][0] + bq.x, f1 = ac[o][0][1] + bq.y, f2 = ac[o][1][0] + bq.z, f3 = ac[o][1][1] + bq.w;
+      if (a.act == 2) { f0 = silu(f0); f1 = silu(f1); f2 = silu(f2); f3 = silu(f3); }
+      const u32x2 out = {pack_bf16(f0, f1), pack_bf16(f2, f3)};
+      if (live && w0 + o < a.OW) {
+        *(u32x2*)(rp + (long)o * a.C) = out;
+        psum[0] += bf_lo(out[0]); psum[1] += bf_hi(out[0]);
+        psum[2] += bf_lo(out[1]); psum[3] += bf_hi(out[1]);
+      }
+      ac[o][0] = ac[o][1] = (f32x2){0.f, 0.f};
+    }
+  };
+
+  u32x2 xc[NJ], xn[NJ];
+  load(0, xc);
+  for (int v0 = 0; v0 < vmax; v0 += P) {
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int v = v0 + u;
+      if (v >= vmax) break;
+      load(v + 1, xn);
+      f32x2 xf[NJ][2];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        xf[j][0] = (f32x2){bf_lo(xc[j][0]), bf_hi(xc[j][0])};
+        xf[j][1] = (f32x2){bf_lo(xc[j][1]), bf_hi(xc[j][1])};
+      }
+#pragma unroll
+      for (int dy = 0; dy < K; ++dy) {
+        if constexpr (true) {
+          if (((u - dy) % S + S) % S != 0) continue;
+          const int slot = (((u - dy + P) / S) % R);
+          const int ol = (v - dy) / S;
+          if (v - dy < 0 || ol >= rows) continue;
+#pragma unroll
+          for (int o = 0; o < SEG; ++o)
+#pragma unroll
+            for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                acc[slot][o][h] = __builtin_elementwise_fma(xf[o * S + dx][h], wt[dy * K + dx][h], acc[slot][o][h]);
+          if (dy == K - 1) finish(acc[slot], ol);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) xc[j] = xn[j];
+    }
+  }
+
+  if (a.pool) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) red[tid * 4 + d] = psum[d];
+    __syncthreads();
+    float* csum = red + 256 * 4;
+    if (tid < CB * 4) {
+      const int c = tid >> 2, d = tid & 3;
+      float sum = 0.f;
+      for (int l = 0; l < SL; ++l) sum += red[(l * CB + c) * 4 + d];   // fixed order
+      csum[tid] = sum;
+    }
+    __syncthreads();
+    const int part = (band * nsb + sb) * ncb + cbk;
+    const int nparts = nbands * nsb * ncb;
+    for (int j = tid; j < a.Cs; j += 256) {
+      const float* w1 = a.w1 + (long)j * a.C + cbk * CB * 4;
+      float h = 0.f;
+      for (int c = 0; c < CB * 4; ++c) h += w1[c] * csum[c];
+      a.pool[((long)b * nparts + part) * a.Cs + j] = h;
+    }
+  }
+}
+
+// Direct-variant plan: CB = widest chunk block dividing C/4; SEG 2 for 5x5, 4 for 3x3;
+// row bands sized for >= 64 workgroups per image (the engine sizes the SE partials per
+// image, so the plan must not depend on the batch).
+static void dwv_plan(const DwkArgs& a, int* cb, int* rb, int* seg, int* ntiles) {
+  const int C4 = a.C / 4;
+  *cb = 0;
+  for (int c : {64, 32, 16, 8})
+    if (C4 % c == 0) { *cb = c; break; }
+  const DwkTile* t = dwk_lookup(a);
+  const bool tab = t != nullptr && t->algo == 2;
+  *seg = a.seg > 0 ? a.seg : tab ? t->seg : (a.K == 5 ? 2 : 4);
+  const int nseg = (a.OW + *seg - 1) / *seg;
+  const int SL = *cb > 0 ? 256 / *cb : 1;
+  const int nsb = (nseg + SL - 1) / SL, ncb = *cb > 0 ? C4 / *cb : 1;
+  int R = a.rb > 0 ? a.rb : tab ? t->rb : 0;
+  if (R <= 0) {
+    int nb = (64 + nsb * ncb - 1) / (nsb * ncb);
+    nb = nb < 1 ? 1 : (nb > a.OH ? a.OH : nb);
+    R = (a.OH + nb - 1) / nb;
+  }
+  *rb = R;
+  *ntiles = ((a.OH + R - 1) / R) * nsb * ncb;
+}
+
+// Which kernel: a.algo, else KDL_DWK_ALGO (A/B runs), else the measured table's choice,
+// else the tiled kernel (tools/dwkbench.py --direct, profiles/dwk_sweep.txt: the direct
+// kernel wins the large-map / stride-2 / 3x3 layers, the tiled one the 5x5 stride-1 layers
+// with many channels, where 25 taps x 8 channels of weights in registers cost occupancy).
+static int dwk_algo(const DwkArgs& a) {
+  int al = a.algo;
+  if (al == 0 && a.cg == 0) {
+    static const int env = [] { const char* e = getenv("KDL_DWK_ALGO"); return e ? atoi(e) : 0; }();
+    al = env;
+  }
+  if (al == 0 && a.cg == 0 && a.lds_kb == 0) {
+    const DwkTile* t = dwk_lookup(a);
+    if (t != nullptr) al = t->algo;
+  }
+  if (al == 0) al = 1;
+  if (al == 2 && a.C % 32 != 0) al = 1;
+  return al;
+}
+
+void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles) {
+  if (dwk_algo(a) == 2) {
+    int seg;
+    dwv_plan(a, cg, rb, &seg, ntiles);
+    *tw = 0;
+    return;
+  }
+  dwt_tiles(a, cg, rb, tw, ntiles);
+}
+
+int dwk_seg(const DwkArgs& a) {
+  if (dwk_algo(a) == 2) {
+    int cb, rb, seg, nt;
+    dwv_plan(a, &cb, &rb, &seg, &nt);
+    return seg;
+  }
+  return dwt_seg(a);
+}
+
+hipError_t dwk(const DwkArgs& a, hipStream_t s) {
+  if (a.C % 8 != 0 || a.B <= 0 || (a.K != 3 && a.K != 5) || (a.S != 1 && a.S != 2)) return hipErrorInvalidValue;
+  if (dwk_algo(a) != 2) return dwt(a, s);
+  int CB, RB, SEG, nt;
+  dwv_plan(a, &CB, &RB, &SEG, &nt);
+  if (CB == 0 || RB <= 0 || (SEG != 2 && SEG != 4)) return hipErrorInvalidValue;
+  const long nblk = (long)a.B * nt;
+  if (nblk >= (1L << 31)) return hipErrorInvalidValue;
+#define KDL_DWV(k, st, sg, cb)                                                                      \
+  if (a.K == k && a.S == st && SEG == sg && CB == cb) {                                           \
+    hipLaunchKernelGGL((dwv_kernel<k, st, sg, cb>), dim3((unsigned)nblk), dim3(256), 0, s, a, RB); \
+    return hipGetLastError();                                                                     \
+  }
+#define KDL_DWV_CB(k, st, sg) KDL_DWV(k, st, sg, 8) KDL_DWV(k, st, sg, 16) KDL_DWV(k, st, sg, 32) KDL_DWV(k, st, sg, 64)
+#define KDL_DWV_KS(k, st) KDL_DWV_CB(k, st, 2) KDL_DWV_CB(k, st, 4)
+  KDL_DWV_KS(3, 1) KDL_DWV_KS(3, 2) KDL_DWV_KS(5, 1) KDL_DWV_KS(5, 2)
+#undef KDL_DWV_KS
+#undef KDL_DWV_CB
+#undef KDL_DWV
   return hipErrorInvalidValue;
 }
 

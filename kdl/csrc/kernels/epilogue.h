@@ -34,8 +34,8 @@ __device__ __noinline__ u32x4 act_transcendental(int mode, u32x4 v) {
       lo = 0.5f * lo * (1.f + erff(lo * 0.70710678118654752f));
       hi = 0.5f * hi * (1.f + erff(hi * 0.70710678118654752f));
     } else {
-      lo = lo / (1.f + __expf(-lo));
-      hi = hi / (1.f + __expf(-hi));
+      lo = fast_silu(lo);
+      hi = fast_silu(hi);
     }
     v[d] = Elt<DT>::pack(lo, hi);
   }

@@ -40,7 +40,7 @@ constexpr int MB_RING = 4;            // parameter blobs in LDS
 
 __device__ __attribute__((aligned(16))) uint8_t mb_zeros[64];
 
-__device__ __forceinline__ float mb_silu(float v) { return v / (1.f + __expf(-v)); }
+__device__ __forceinline__ float mb_silu(float v) { return fast_silu(v); }
 
 __device__ __forceinline__ void mb_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ void mb_wait_vm(int n) {

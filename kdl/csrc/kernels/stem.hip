@@ -103,8 +103,8 @@ __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
       if (a.relu == 1) {
         v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       } else if (a.relu == 2) {
-        v0 = v0 / (1.f + __expf(-v0)); v1 = v1 / (1.f + __expf(-v1));
-        v2 = v2 / (1.f + __expf(-v2)); v3 = v3 / (1.f + __expf(-v3));
+        v0 = fast_silu(v0); v1 = fast_silu(v1);
+        v2 = fast_silu(v2); v3 = fast_silu(v3);
       }
       *(u32x2*)(ys + ml * NF * 16 + n) = (u32x2){E::pack(v0, v1), E::pack(v2, v3)};
     }

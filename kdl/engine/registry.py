@@ -85,6 +85,24 @@ _FACTORIES = {"xception": _xception, "resnet50": _resnet50, "resnet50_bf16": lam
               "vit_b16": _vit_b16, "vit_b16_fp8": _vit_b16_fp8, "efficientnet_b7": _efficientnet_b7}
 
 
+# (family, --dtype) -> engine variant; "auto" keeps the family's own default
+_VARIANTS = {("resnet50", "bf16"): "resnet50_bf16", ("resnet50_bf16", "fp16"): "resnet50",
+             ("vit_b16", "fp8"): "vit_b16_fp8", ("vit_b16_fp8", "bf16"): "vit_b16"}
+_DTYPES = {"xception": {"bf16"}, "resnet50": {"fp16"}, "resnet50_bf16": {"bf16"}, "vit_b16": {"bf16"},
+           "vit_b16_fp8": {"fp8"}, "efficientnet_b7": {"bf16"}}
+
+
+def variant(family: str, dtype: str = "auto") -> str:
+    """The engine variant of `family` computing in `dtype` (server ``--dtype``)."""
+    if dtype in ("auto", "") or dtype in _DTYPES.get(family, set()):
+        return family
+    v = _VARIANTS.get((family, dtype))
+    if v is None:
+        raise ValueError(f"{family} has no {dtype} engine (available: "
+                         f"{sorted(_DTYPES.get(family, set()) | {d for (f, d) in _VARIANTS if f == family})})")
+    return v
+
+
 def models() -> list[str]:
     return sorted(_FACTORIES)
 

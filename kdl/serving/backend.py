@@ -285,16 +285,19 @@ class GPUExecutor(_Executor):
         r = self.runner
         src = r.source
         bs = r.buckets
+        fam = registry.variant(src.family, r.cfg.dtype)      # --dtype picks the engine variant
+        cap = bool(self.engine_kwargs.get("graph", True))      # --graph off: eager launches
         in_kind = "u8" if r.sig.input_dtype == P.DT_UINT8 else "f32"
         dev = f"cuda:{self.device}"
         def make(b, buckets=None):
-            if src.family == "xception":
+            if fam == "xception":
                 from ..engine.xception import XceptionEngine
                 return XceptionEngine(src.params, max_batch=b, device=dev, in_kind=in_kind,
                                       head=src.head, buckets=buckets)
-            return registry.get(src.family).engine(src.params, b, dev, buckets=buckets)
+            return registry.get(fam).engine(src.params, b, dev, buckets=buckets)
         self.engine = make(bs[-1], bs)
-        tp = tuning_path(src.family, bs[-1])
+        info = registry.get(fam)
+        tp = tuning_path(info.tuning or fam, bs[-1])
         if tp.exists():
             self.engine.load_tuning(tp)
         # KDL_LANES=2: full batches of the top bucket run as concurrent split-batch
@@ -303,21 +306,21 @@ class GPUExecutor(_Executor):
         # batch per executor) and the extra graph launch + fork/join cost 4 % at
         # 16 clients x 8 images (profiles/serve_lanes_ab.txt), unlike bench.py.
         self.lanes = None
-        nl = int(self.engine_kwargs.get("lanes", os.environ.get("KDL_LANES", "1")))
+        nl = int(self.engine_kwargs.get("lanes") or os.environ.get("KDL_LANES", "1"))
         if nl > 1 and bs[-1] % nl == 0 and bs[-1] // nl >= 4:
             from ..engine.lanes import LaneGroup
             self.lanes = LaneGroup(None, None, bs[-1], dev, nl, make=make)
             if tp.exists():
                 self.lanes.load_tuning(tp)
-            self.lanes.program(bs[-1], capture=True)
-            self.lanes.launch(bs[-1])
+            self.lanes.program(bs[-1], capture=cap)
+            self.lanes.launch(bs[-1], capture=cap)
         # stage pipelining of full top-bucket batches (kdl/engine/stages.py): stage 1 of
         # batch n+1 overlaps stage 2 of batch n. Default: the family's cut (Xception:
         # after block7_sepconv1) unless lanes were asked for; KDL_STAGES=none disables.
         self.pipe = None
-        cut = self.engine_kwargs.get("stages", os.environ.get("KDL_STAGES", ""))
+        cut = self.engine_kwargs.get("stages") or os.environ.get("KDL_STAGES", "")
         if not cut:
-            cut = registry.get(src.family).stage_cut
+            cut = info.stage_cut
         if cut and cut != "none" and self.lanes is None and hasattr(self.engine, "alias_buffer"):
             from ..engine.stages import StagePipe
             self.pipe = StagePipe(make(bs[-1]), cut)
@@ -326,7 +329,8 @@ class GPUExecutor(_Executor):
         # pipelining depth (batches in flight per GPU): staging / output slots, each with
         # its own captured graphs (engine input slots), so the host can form batch n+1
         # while batch n runs
-        self.depth = max(1, int(self.engine_kwargs.get("depth", os.environ.get("KDL_EXEC_DEPTH", "2"))))
+        self.depth = max(1, int(self.engine_kwargs.get("depth") or os.environ.get("KDL_EXEC_DEPTH", "2")))
+        self.capture = cap
         for e in (self.engine, self.lanes, self.pipe):
             if e is not None:
                 e.add_input_slots(self.depth)
@@ -341,12 +345,12 @@ class GPUExecutor(_Executor):
         self._rt = _lib.lib()
         for slot in range(self.depth):        # warm-up + capture one hipGraph per (bucket, slot)
             for bk in bs:
-                self.engine.program(bk, capture=True, slot=slot)
-                self.engine.launch(bk, slot=slot)
+                self.engine.program(bk, capture=cap, slot=slot)
+                self.engine.launch(bk, capture=cap, slot=slot)
             for big in (self.lanes, self.pipe):
                 if big is not None:
-                    big.program(bs[-1], capture=True, slot=slot)
-                    big.launch(bs[-1], slot=slot)
+                    big.program(bs[-1], capture=cap, slot=slot)
+                    big.launch(bs[-1], capture=cap, slot=slot)
         torch.cuda.synchronize(self.device)
 
     def staging_ptr(self, slot: int = 0) -> int:
@@ -364,11 +368,11 @@ class GPUExecutor(_Executor):
         C.memcpy_async(inp.data_ptr(), stg.data_ptr(), nbytes, 1, self.copy_stream.cuda_stream)
         self.h2d_done[slot].record(self.copy_stream)
         if e is self.pipe:                    # free-running stages; logits final on stage 2's stream
-            e.launch_async(bucket, [self.h2d_done[slot]], [self.done[slot]], slot=slot)
+            e.launch_async(bucket, [self.h2d_done[slot]], [self.done[slot]], capture=self.capture, slot=slot)
             out_stream = e.out_stream
         else:
             e.stream.wait_event(self.h2d_done[slot])
-            e.launch(bucket, e.stream, slot=slot)
+            e.launch(bucket, e.stream, capture=self.capture, slot=slot)
             out_stream = e.stream
         lg = e.slot_logits(slot)
         C.memcpy_async(self.out[slot].data_ptr(), lg.data_ptr(), bucket * lg.shape[1] * 4, 2, out_stream.cuda_stream)
@@ -435,7 +439,7 @@ class SignatureRunner:
         if devices:
             for d in devices:
                 for _ in range(max(1, cfg.executors_per_gpu)):
-                    self.executors.append(GPUExecutor(self, d, {}))
+                    self.executors.append(GPUExecutor(self, d, cfg.engine_kwargs()))
         else:
             for i in range(max(1, cfg.executors_per_gpu)):
                 self.executors.append(CPUExecutor(self, i))

@@ -58,6 +58,15 @@ class ServerConfig:
     synthetic: bool = False       # random-init weights when the repo has no artifact
     labels: list[str] = field(default_factory=list)
     host: str = "0.0.0.0"
+    # MI355X-native engine knobs (SURVEY.md §5 "Config / flag system")
+    dtype: str = "auto"           # auto | bf16 | fp16 | fp8: picks the family's engine variant
+    graph: bool = True            # hipGraph replay per (bucket, slot); off = eager kernel launches
+    stages: str = ""              # stage-pipeline cut ("" = the family's default, "none" = off)
+    lanes: int = 1                # split-batch hipGraph lanes for the top bucket
+    exec_depth: int = 2           # batches in flight per GPU executor
+
+    def engine_kwargs(self) -> dict:
+        return {"graph": self.graph, "stages": self.stages, "lanes": self.lanes, "depth": self.exec_depth}
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -80,6 +89,15 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--allowed_batch_sizes", default=None, help="comma separated, e.g. 1,4,8,16,32")
     ap.add_argument("--synthetic_model", action="store_true")
     ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--dtype", choices=["auto", "bf16", "fp16", "fp8"], default="auto",
+                    help="compute dtype: selects the family's engine variant (resnet50: fp16 | bf16; "
+                         "vit_b16: bf16 | fp8 e4m3 linears; xception / efficientnet_b7: bf16)")
+    ap.add_argument("--graph", choices=["on", "off"], default="on",
+                    help="replay one captured hipGraph per (batch bucket, slot); off = eager launches")
+    ap.add_argument("--stages", default=None,
+                    help="stage-pipeline cut step (default: the family's; 'none' disables)")
+    ap.add_argument("--lanes", type=int, default=None, help="split-batch hipGraph lanes (top bucket)")
+    ap.add_argument("--exec_depth", type=int, default=None, help="batches in flight per GPU executor")
     return ap
 
 
@@ -111,4 +129,7 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         grpc_max_threads=a.grpc_max_threads, rest_api_num_threads=a.rest_api_num_threads,
                         device=a.device, gpus=a.gpus, executors_per_gpu=a.executors_per_gpu,
                         synthetic=a.synthetic_model or _truthy(env.get("KDL_SYNTHETIC_MODEL", "0")),
-                        labels=labels, host=a.host)
+                        labels=labels, host=a.host, dtype=a.dtype, graph=a.graph == "on",
+                        stages=a.stages if a.stages is not None else env.get("KDL_STAGES", ""),
+                        lanes=a.lanes if a.lanes is not None else int(env.get("KDL_LANES", "1")),
+                        exec_depth=a.exec_depth if a.exec_depth is not None else int(env.get("KDL_EXEC_DEPTH", "2")))

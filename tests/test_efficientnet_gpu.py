@@ -24,7 +24,11 @@ def _rel(a, b):
     (5, 2, 38, 1344, None), (3, 1, 19, 2304, None),
     (3, 2, 75, 480, dict(cg=4, rb=8, tw=19, seg=3)), (5, 2, 38, 960, dict(cg=8, rb=3, tw=7, seg=7)),
     (5, 1, 38, 960, dict(cg=2, rb=5, tw=13, seg=8)), (3, 1, 37, 64, dict(cg=1, rb=16, tw=37, seg=4)),
-    (3, 2, 37, 64, dict(cg=8, rb=1, tw=5, seg=5))])
+    (3, 2, 37, 64, dict(cg=8, rb=1, tw=5, seg=5)),
+    # direct streaming kernel (algo 2): every (K, S), both SEGs, ragged row bands, CB 8..64
+    (3, 1, 37, 64, dict(algo=2, seg=4, rb=5)), (3, 2, 75, 288, dict(algo=2, seg=2, rb=7)),
+    (5, 1, 19, 1344, dict(algo=2, seg=2, rb=19)), (5, 2, 38, 960, dict(algo=2, seg=4, rb=3)),
+    (5, 1, 38, 2304, dict(algo=2, seg=4, rb=0)), (3, 1, 16, 32, dict(algo=2, seg=2, rb=1))])
 def test_dwk_silu_and_fused_squeeze_excite(K, S, H, C, tile):
     gen = torch.Generator().manual_seed(K * 100 + S * 10 + H)
     B, Cs = 2, max(1, C // 24)

@@ -1,0 +1,51 @@
+"""Model-server flag parsing (SURVEY.md §5 "Config / flag system"): TF-Serving flags and
+env (tf-serving.dockerfile:2-5 entrypoint), the batching-parameters text proto, and the
+MI355X-native engine knobs (--dtype variant selection, --graph, --stages, --lanes,
+--exec_depth)."""
+import pytest
+
+from kdl.engine import registry
+from kdl.serving.config import BatchingParams, config_from_args
+
+
+def test_tf_serving_flags_and_env():
+    c = config_from_args(["--port", "9000", "--rest_api_port", "9001"],
+                         env={"MODEL_NAME": "clothing-model", "MODEL_BASE_PATH": "/m"})
+    assert (c.port, c.rest_api_port, c.model_name, c.model_base_path) == (9000, 9001, "clothing-model",
+                                                                          "/m/clothing-model")
+    assert c.enable_batching and c.graph and c.dtype == "auto"
+
+
+def test_batching_parameters_text_proto(tmp_path):
+    p = tmp_path / "batching.txt"
+    p.write_text("max_batch_size { value: 16 }\nbatch_timeout_micros { value: 500 }\n"
+                 "allowed_batch_sizes: 4\nallowed_batch_sizes: 16\n")
+    c = config_from_args(["--batching_parameters_file", str(p)], env={})
+    assert c.batching.max_batch_size == 16 and c.batching.batch_timeout_micros == 500
+    assert c.batching.allowed_batch_sizes == [4, 16]
+    assert BatchingParams.parse("max_batch_size { value: 8 }").allowed_batch_sizes == [1, 2, 4, 8]
+
+
+def test_native_engine_flags():
+    c = config_from_args(["--dtype", "fp8", "--graph", "off", "--stages", "none", "--lanes", "2",
+                          "--exec_depth", "3"], env={})
+    assert c.dtype == "fp8" and not c.graph
+    assert c.engine_kwargs() == {"graph": False, "stages": "none", "lanes": 2, "depth": 3}
+    # env fallbacks of the same knobs
+    c = config_from_args([], env={"KDL_STAGES": "block7_sepconv1", "KDL_LANES": "2", "KDL_EXEC_DEPTH": "4"})
+    assert c.engine_kwargs() == {"graph": True, "stages": "block7_sepconv1", "lanes": 2, "depth": 4}
+
+
+def test_dtype_selects_engine_variant():
+    assert registry.variant("resnet50", "auto") == "resnet50"
+    assert registry.variant("resnet50", "fp16") == "resnet50"
+    assert registry.variant("resnet50", "bf16") == "resnet50_bf16"
+    assert registry.variant("vit_b16", "fp8") == "vit_b16_fp8"
+    assert registry.variant("vit_b16_fp8", "bf16") == "vit_b16"
+    assert registry.variant("xception", "bf16") == "xception"
+    for fam in registry.models():
+        assert registry.variant(fam, "auto") == fam
+    with pytest.raises(ValueError):
+        registry.variant("xception", "fp8")
+    with pytest.raises(SystemExit):
+        config_from_args(["--dtype", "int4"], env={})

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--grid", action="store_true", help="also sweep explicit (cg, rb, tw, seg) tiles")
     ap.add_argument("--max-lds", type=int, default=96)
+    ap.add_argument("--direct", action="store_true", help="sweep the direct streaming kernel (algo 2) only")
     a = ap.parse_args()
     C_ = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -81,15 +82,31 @@ def main():
         print(f"{name:4s} {H}x{W}x{C} k{K}s{S} x{nl}: auto {t0:7.1f} us {gb / t0 * 1e3:5.2f} TB/s err {e:.1e} "
               f"tiles {C_.dwk_tiles(base)}", flush=True)
         assert e < 2e-2, e
-        for kb in (16, 24, 32, 40, 48, 64, 80, 96):
+        for alg in (1, 2):
+            t, e = tm(dict(algo=alg))
+            assert e < 2e-2, (alg, e)
+            print(f"      algo {alg} (default tiles {C_.dwk_tiles({**base, 'algo': alg})}): {t:7.1f} us "
+                  f"{gb / t * 1e3:5.2f} TB/s", flush=True)
+        if a.direct:
+            for seg in (2, 4):
+                for rb in (0, 2, 4, 6, 8, 12, 16, 24, 38, 75):
+                    if rb > OH:
+                        continue
+                    kw = dict(algo=2, seg=seg, rb=rb)
+                    if not ok(kw):
+                        continue
+                    t, e = tm(kw)
+                    assert e < 2e-2, (kw, e)
+                    res.append((t, kw, C_.dwk_tiles({**base, **kw})[:3]))
+        for kb in (() if a.direct else (16, 24, 32, 40, 48, 64, 80, 96)):
             for seg in (3, 4, 5, 7):
-                kw = dict(lds_kb=kb, seg=seg)
+                kw = dict(lds_kb=kb, seg=seg, algo=1)
                 if not ok(kw):
                     continue
                 t, e = tm(kw)
                 assert e < 2e-2, (kw, e)
                 res.append((t, kw, C_.dwk_tiles({**base, **kw})[:3]))
-        if a.grid:
+        if a.grid and not a.direct:
             C8 = C // 8
             tws = sorted({(OW + k - 1) // k for k in range(1, 9)} - {0})
             for cg in [d for d in (1, 2, 4, 8) if C8 % d == 0]:
@@ -106,10 +123,12 @@ def main():
                             t, e = tm(kw, 10)
                             assert e < 2e-2, (kw, e)
                             res.append((t, kw, (cg, rb, tw)))
+        if not res:
+            res.append((t0, {}, None))
         res.sort(key=lambda r: r[0])
         for t, kw, tiles in res[:6]:
-            print(f"      {t:7.1f} us {gb / t * 1e3:5.2f} TB/s  {kw} tiles(cg,rb,tw)={tiles} "
-                  f"smem {smem(K, S, *tiles) // 1024} KiB", flush=True)
+            lds = f"smem {smem(K, S, *tiles) // 1024} KiB" if kw.get("algo") == 1 else ""
+            print(f"      {t:7.1f} us {gb / t * 1e3:5.2f} TB/s  {kw} tiles={tiles} {lds}", flush=True)
         tot_auto += t0 * nl
         tot_best += res[0][0] * nl
     print(f"B7 depthwise total over the listed shapes (x layers): auto {tot_auto:.0f} us, best {tot_best:.0f} us")
