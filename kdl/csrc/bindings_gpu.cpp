@@ -116,7 +116,7 @@ DwkArgs dwk_args(const py::dict& d) {
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.C = I(d, "C"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
   a.K = I(d, "K"); a.S = I(d, "S", 1); a.pad = I(d, "pad"); a.act = I(d, "act"); a.Cs = I(d, "Cs");
   a.cg = I(d, "cg", 0); a.rb = I(d, "rb", 0); a.tw = I(d, "tw", 0); a.seg = I(d, "seg", 0);
-  a.lds_kb = I(d, "lds_kb", 0); a.algo = I(d, "algo", 0);
+  a.lds_kb = I(d, "lds_kb", 0); a.algo = I(d, "algo", 0); a.pd = I(d, "pd", 0);
   return a;
 }
 SeArgs se_args(const py::dict& d) {

@@ -205,7 +205,7 @@ static size_t dwk_smem(int K, int S, int CG, int RB, int TW) {
 // 25 % slower summed over B7) -- keep the CG with the tallest band, ties -> wider CG.
 // SEG odd: the items of a wave then start on different LDS bank slots (stride 2: with the
 // patch column-deinterleaved). a.cg/rb/tw/seg override everything.
-struct DwkTile { short H, W, C, K, S, algo, cg, rb, tw, seg; };   // algo 2: rb / seg of dwv_kernel
+struct DwkTile { short H, W, C, K, S, algo, cg, rb, tw, seg; };   // algo 2: rb / seg of dwv_kernel, tw = prefetch rows
 static const DwkTile kDwkTable[] = {
     {300, 300, 64, 3, 1, 2, 0, 16, 0, 4},   {300, 300, 32, 3, 1, 2, 0, 16, 0, 2},  {300, 300, 192, 3, 2, 2, 0, 6, 0, 2},
     {150, 150, 288, 3, 1, 2, 0, 38, 0, 2},  {150, 150, 288, 5, 2, 2, 0, 16, 0, 4}, {75, 75, 480, 5, 1, 1, 4, 8, 38, 5},
@@ -288,7 +288,7 @@ static hipError_t dwt(const DwkArgs& a, hipStream_t s) {
 // overlap its own arithmetic and its LDS budget caps the CU at 1-3 workgroups.
 // Workgroup = CB chunk lanes x (256/CB) segment lanes of one (image, row band); the SE
 // partials are per workgroup (part = band x segment block x chunk block).
-template <int K, int S, int SEG, int CB>
+template <int K, int S, int SEG, int CB, int PD>
 __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
   constexpr int R = (K + S - 1) / S;       // output rows in flight
   constexpr int P = R * S;                 // unroll period (input rows)
@@ -362,19 +362,22 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
     }
   };
 
-  u32x2 xc[NJ], xn[NJ];
-  load(0, xc);
+  // rows v .. v+PD-1 are in registers (xq[0] = row v) and row v+PD is issued at the top of
+  // step v: PD rows of arithmetic cover each load's latency
+  u32x2 xq[PD + 1][NJ];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) load(k, xq[k]);
   for (int v0 = 0; v0 < vmax; v0 += P) {
 #pragma unroll
     for (int u = 0; u < P; ++u) {
       const int v = v0 + u;
       if (v >= vmax) break;
-      load(v + 1, xn);
+      load(v + PD, xq[PD]);
       f32x2 xf[NJ][2];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        xf[j][0] = (f32x2){bf_lo(xc[j][0]), bf_hi(xc[j][0])};
-        xf[j][1] = (f32x2){bf_lo(xc[j][1]), bf_hi(xc[j][1])};
+        xf[j][0] = (f32x2){bf_lo(xq[0][j][0]), bf_hi(xq[0][j][0])};
+        xf[j][1] = (f32x2){bf_lo(xq[0][j][1]), bf_hi(xq[0][j][1])};
       }
 #pragma unroll
       for (int dy = 0; dy < K; ++dy) {
@@ -394,7 +397,9 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) xc[j] = xn[j];
+      for (int k = 0; k < PD; ++k)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) xq[k][j] = xq[k + 1][j];
     }
   }
 
@@ -488,20 +493,24 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
   if (dwk_algo(a) != 2) return dwt(a, s);
   int CB, RB, SEG, nt;
   dwv_plan(a, &CB, &RB, &SEG, &nt);
-  if (CB == 0 || RB <= 0 || (SEG != 2 && SEG != 4)) return hipErrorInvalidValue;
+  const DwkTile* tb = dwk_lookup(a);
+  const int PDv = a.pd > 0 ? a.pd : (tb != nullptr && tb->algo == 2 && tb->tw > 0) ? tb->tw : 1;
+  if (CB == 0 || RB <= 0 || (SEG != 2 && SEG != 4) || (PDv != 1 && PDv != 3)) return hipErrorInvalidValue;
   const long nblk = (long)a.B * nt;
   if (nblk >= (1L << 31)) return hipErrorInvalidValue;
-#define KDL_DWV(k, st, sg, cb)                                                                      \
-  if (a.K == k && a.S == st && SEG == sg && CB == cb) {                                           \
-    hipLaunchKernelGGL((dwv_kernel<k, st, sg, cb>), dim3((unsigned)nblk), dim3(256), 0, s, a, RB); \
-    return hipGetLastError();                                                                     \
+#define KDL_DWV1(k, st, sg, cb, pd)                                                                     \
+  if (a.K == k && a.S == st && SEG == sg && CB == cb && PDv == pd) {                                  \
+    hipLaunchKernelGGL((dwv_kernel<k, st, sg, cb, pd>), dim3((unsigned)nblk), dim3(256), 0, s, a, RB); \
+    return hipGetLastError();                                                                         \
   }
+#define KDL_DWV(k, st, sg, cb) KDL_DWV1(k, st, sg, cb, 1) KDL_DWV1(k, st, sg, cb, 3)
 #define KDL_DWV_CB(k, st, sg) KDL_DWV(k, st, sg, 8) KDL_DWV(k, st, sg, 16) KDL_DWV(k, st, sg, 32) KDL_DWV(k, st, sg, 64)
 #define KDL_DWV_KS(k, st) KDL_DWV_CB(k, st, 2) KDL_DWV_CB(k, st, 4)
   KDL_DWV_KS(3, 1) KDL_DWV_KS(3, 2) KDL_DWV_KS(5, 1) KDL_DWV_KS(5, 2)
 #undef KDL_DWV_KS
 #undef KDL_DWV_CB
 #undef KDL_DWV
+#undef KDL_DWV1
   return hipErrorInvalidValue;
 }
 

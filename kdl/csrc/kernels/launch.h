@@ -208,6 +208,7 @@ struct DwkArgs {
   int cg, rb, tw, seg;    // tile override (0: host heuristic; tools/dwkbench.py sweeps these)
   int lds_kb;             // heuristic's LDS budget per workgroup (0: default)
   int algo;               // 0 auto, 1 LDS-tiled, 2 direct streaming (dwv_kernel)
+  int pd;                 // dwv_kernel: input rows prefetched ahead (0: table / 1)
 };
 hipError_t dwk(const DwkArgs& a, hipStream_t s);
 void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles);

@@ -37,7 +37,7 @@ def test_layernorm_rows_and_strided_cls_rows():
     assert _rel(cls[:B], ref.view(B, T, D)[:, 0]) < 1e-2
 
 
-@pytest.mark.parametrize("T", [197, 50])
+@pytest.mark.parametrize("T", [197, 50, 256, 300, 1])   # <= 256: whole-head kernel; 300: query-tiled
 def test_attention_matches_softmax_reference(T):
     gen = torch.Generator().manual_seed(T)
     B, H, dh = 2, 12, 64

@@ -88,11 +88,10 @@ def main():
             print(f"      algo {alg} (default tiles {C_.dwk_tiles({**base, 'algo': alg})}): {t:7.1f} us "
                   f"{gb / t * 1e3:5.2f} TB/s", flush=True)
         if a.direct:
-            for seg in (2, 4):
-                for rb in (0, 2, 4, 6, 8, 12, 16, 24, 38, 75):
+            for seg, rb, pd in [(sg, r, p) for sg in (2, 4) for r in (0, 4, 8, 12, 16, 24, 38, 75) for p in (1, 3)]:
                     if rb > OH:
                         continue
-                    kw = dict(algo=2, seg=seg, rb=rb)
+                    kw = dict(algo=2, seg=seg, rb=rb, pd=pd)
                     if not ok(kw):
                         continue
                     t, e = tm(kw)

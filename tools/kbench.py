@@ -34,6 +34,11 @@ SHAPES = {
     # core-efficiency probes (large square GEMMs; M = batch*64*64)
     "sq4k": (MODE_PW, 4096, 4096, 64, 1),
     "sq2k": (MODE_PW, 2048, 2048, 64, 1),
+    # ViT-B/16 linears (M = 32 x 14 x 14 = 6272 rows ~ the engine's 32 x 197 = 6304)
+    "vit_qkv": (MODE_PW, 768, 2304, 14, 1),
+    "vit_proj": (MODE_PW, 768, 768, 14, 1),
+    "vit_mlp0": (MODE_PW, 768, 3072, 14, 1),
+    "vit_mlp3": (MODE_PW, 3072, 768, 14, 1),
 }
 
 
