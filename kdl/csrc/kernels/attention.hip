@@ -98,26 +98,27 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       }
     }
     float tmax = -INFINITY;
+    const bool full = (kt + 1) * AT_KV <= a.T;     // only the last key tile needs the mask
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt * AT_KV + 16 * kf + 4 * q + r;
-        const float v = key < a.T ? s[kf][r] * sl2 : -INFINITY;
+        const float v = (full || key < a.T) ? s[kf][r] * sl2 : -INFINITY;
         s[kf][r] = v;
         tmax = fmaxf(tmax, v);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
     const float mn = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
     m = mn;
     float ls = 0.f;
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kf][r] - mn);
+        const float p = __builtin_amdgcn_exp2f(s[kf][r] - mn);
         s[kf][r] = p;
         ls += p;
       }
@@ -127,12 +128,10 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     // O^T[dim 16df + 4q + r][query c] += V^T P^T
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      s16x8 pb;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pb[r] = (short)f2bf(s[2 * k2][r]);
-        pb[4 + r] = (short)f2bf(s[2 * k2 + 1][r]);
-      }
+      const u32x4 pw = {pack_bf16(s[2 * k2][0], s[2 * k2][1]), pack_bf16(s[2 * k2][2], s[2 * k2][3]),
+                        pack_bf16(s[2 * k2 + 1][0], s[2 * k2 + 1][1]),
+                        pack_bf16(s[2 * k2 + 1][2], s[2 * k2 + 1][3])};
+      const s16x8 pb = __builtin_bit_cast(s16x8, pw);
 #pragma unroll
       for (int df = 0; df < 4; ++df) {
         const uint16_t* vr = vt + (16 * df + c) * AT_ROW + 32 * k2 + 4 * q;
@@ -231,26 +230,27 @@ __global__ __launch_bounds__(1024) void attn_head_kernel(AttnArgs a) {
       }
     }
     float tmax = -INFINITY;
+    const bool full = (kt + 1) * AT_KV <= a.T;     // only the last key tile needs the mask
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kt * AT_KV + 16 * kf + 4 * q + r;
-        const float v = key < a.T ? s[kf][r] * sl2 : -INFINITY;
+        const float v = (full || key < a.T) ? s[kf][r] * sl2 : -INFINITY;
         s[kf][r] = v;
         tmax = fmaxf(tmax, v);
       }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
     const float mn = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
     m = mn;
     float ls = 0.f;
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s[kf][r] - mn);
+        const float p = __builtin_amdgcn_exp2f(s[kf][r] - mn);
         s[kf][r] = p;
         ls += p;
       }
@@ -259,12 +259,10 @@ __global__ __launch_bounds__(1024) void attn_head_kernel(AttnArgs a) {
     for (int d = 0; d < 4; ++d) o[d] *= alpha;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
-      s16x8 pb;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pb[r] = (short)f2bf(s[2 * k2][r]);
-        pb[4 + r] = (short)f2bf(s[2 * k2 + 1][r]);
-      }
+      const u32x4 pw = {pack_bf16(s[2 * k2][0], s[2 * k2][1]), pack_bf16(s[2 * k2][2], s[2 * k2][3]),
+                        pack_bf16(s[2 * k2 + 1][0], s[2 * k2 + 1][1]),
+                        pack_bf16(s[2 * k2 + 1][2], s[2 * k2 + 1][3])};
+      const s16x8 pb = __builtin_bit_cast(s16x8, pw);
 #pragma unroll
       for (int df = 0; df < 4; ++df) {
         const uint16_t* vr = vt + (16 * df + c) * AW_VROW + kt * AT_KV + 32 * k2 + 4 * q;
