@@ -139,8 +139,76 @@ __global__ __launch_bounds__(256) void layernorm_kernel(LnArgs a) {
   }
 }
 
+// Two rows per wave (32 lanes per row, up to 4 chunks of 8 per lane: D <= 1024): every lane
+// is busy at D = 768 (the kernel above leaves half its lanes idle for a row's second chunk),
+// and sum / sum of squares reduce together in one 5-step butterfly instead of two dependent
+// 6-step ones (the row's statistics were a chain of 12 ds_bpermute latencies).
+__global__ __launch_bounds__(256) void layernorm2_kernel(LnArgs a) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, hl = lane & 31;
+  const long r = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + half;
+  const bool live = r < a.rows;
+  const uint16_t* xr = a.x + (live ? r : 0) * a.ldx;
+  const int C8 = a.D / 8;
+  float v[LN_CH][8];
+  float s = 0.f, ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < LN_CH; ++j) {
+    const int c8 = hl + 32 * j;
+    u32x4 u = {0u, 0u, 0u, 0u};
+    if (live && c8 < C8) u = *(const u32x4*)(xr + c8 * 8);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      v[j][2 * d] = bf_lo(u[d]);
+      v[j][2 * d + 1] = bf_hi(u[d]);
+    }
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      s += v[j][d];
+      ss += v[j][d] * v[j][d];
+    }
+  }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    ss += __shfl_xor(ss, off);
+  }
+  const float inv_d = 1.f / (float)a.D;
+  const float mean = s * inv_d;
+  const float var = fmaxf(ss * inv_d - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + a.eps);
+  if (!live) return;
+  uint16_t* yr = a.y + r * a.ldy;
+#pragma unroll
+  for (int j = 0; j < LN_CH; ++j) {
+    const int c8 = hl + 32 * j;
+    if (c8 < C8) {
+      const float4 g0 = *(const float4*)(a.gamma + c8 * 8), g1 = *(const float4*)(a.gamma + c8 * 8 + 4);
+      const float4 b0 = *(const float4*)(a.beta + c8 * 8), b1 = *(const float4*)(a.beta + c8 * 8 + 4);
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      float o8[8];
+#pragma unroll
+      for (int d = 0; d < 8; ++d) o8[d] = (v[j][d] - mean) * rstd * g[d] + bb[d];
+      if (a.y8) {
+        const float q = a.inv_scale;
+        *(u32x2*)(a.y8 + r * a.ldy + c8 * 8) = (u32x2){pack_fp8x4(o8[0] * q, o8[1] * q, o8[2] * q, o8[3] * q),
+                                                        pack_fp8x4(o8[4] * q, o8[5] * q, o8[6] * q, o8[7] * q)};
+      } else {
+        u32x4 o;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = pack_bf16(o8[2 * d], o8[2 * d + 1]);
+        *(u32x4*)(yr + c8 * 8) = o;
+      }
+    }
+  }
+}
+
 hipError_t layernorm(const LnArgs& a, hipStream_t s) {
   if (a.D % 8 != 0 || a.D > 64 * 8 * LN_CH || a.rows <= 0) return hipErrorInvalidValue;
+  if (a.D <= 32 * 8 * LN_CH) {
+    hipLaunchKernelGGL(layernorm2_kernel, dim3((unsigned)((a.rows + 7) / 8)), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((a.rows + 3) / 4)), dim3(256), 0, s, a);
   return hipGetLastError();
 }

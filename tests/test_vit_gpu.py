@@ -18,9 +18,10 @@ def _rel(a, b):
     return ((a.float().cpu() - b.float().cpu()).abs().max() / b.float().abs().max()).item()
 
 
-def test_layernorm_rows_and_strided_cls_rows():
+@pytest.mark.parametrize("D", [768, 200, 2048])   # <= 1024: two rows per wave; 2048: one row per wave
+def test_layernorm_rows_and_strided_cls_rows(D):
     gen = torch.Generator().manual_seed(0)
-    B, T, D = 3, 197, 768
+    B, T = 3, 197
     x = (torch.randn(B * T, D, generator=gen) * 2 + 0.5).to(torch.bfloat16).to(DEV)
     g = torch.rand(D, generator=gen).to(DEV) + 0.5
     b = torch.randn(D, generator=gen).to(DEV) * 0.1
