@@ -31,8 +31,8 @@ __device__ __noinline__ u32x4 act_transcendental(int mode, u32x4 v) {
   for (int d = 0; d < 4; ++d) {
     float lo = Elt<DT>::lo(v[d]), hi = Elt<DT>::hi(v[d]);
     if (mode == 3) {
-      lo = 0.5f * lo * (1.f + erff(lo * 0.70710678118654752f));
-      hi = 0.5f * hi * (1.f + erff(hi * 0.70710678118654752f));
+      lo = 0.5f * lo * (1.f + fast_erf(lo * 0.70710678118654752f));
+      hi = 0.5f * hi * (1.f + fast_erf(hi * 0.70710678118654752f));
     } else {
       lo = fast_silu(lo);
       hi = fast_silu(hi);
