@@ -62,6 +62,7 @@ StemArgs stem_args(const py::dict& d) {
   const char* sk[3] = {"scale0", "scale1", "scale2"};
   const char* hk[3] = {"shift0", "shift1", "shift2"};
   for (int c = 0; c < 3; ++c) { a.scale[c] = F(d, sk[c], 1.f); a.shift[c] = F(d, hk[c], 0.f); }
+  a.rows = I(d, "rows", 0);
   return a;
 }
 GapArgs gap_args(const py::dict& d) {

@@ -101,6 +101,8 @@ struct StemArgs {
                                   // stays exact: padded taps are 0 in the normalised space)
   int relu;                       // 0 none, 1 ReLU, 2 SiLU
   int dt;                         // output element type: 0 bf16, 1 fp16
+  int rows;                       // 1: row-run K layout (k = ky*RP + kx*3 + c, RP = 32 for 7x7,
+                                  // 16 for 3x3; stem_rows_kernel); 0: k = (ky*KW+kx)*3 + c
 };
 hipError_t stem_conv(const StemArgs& a, hipStream_t s);
 

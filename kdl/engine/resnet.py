@@ -18,6 +18,7 @@ at batch 32, well inside one MI355X's 288 GB and mostly MALL-resident).
 """
 from __future__ import annotations
 
+import os
 from pathlib import Path
 
 import torch
@@ -25,7 +26,7 @@ import torch
 from ..models import resnet as R
 from ..ops import _lib
 from ..ops.conv import MODE_CONV, MODE_PW, ConvGemmLayer, Geometry
-from ..ops.pack import pack_fragments
+from ..ops.pack import pack_fragments, rowrun_weights
 from .base import EngineBase, Step
 
 
@@ -66,9 +67,15 @@ class ResNetEngine(EngineBase):
     def _build(self, p: dict) -> None:
         dev = self.device
         S = self.size
-        # stem: 7x7/2 pad 3, K = 147 (k = tap*3 + c) padded to 160
+        # stem: 7x7/2 pad 3. uint8 input: row-run K layout (k = ky*32 + kx*3 + c, K = 224:
+        # each lane's 8 k-slots are 8 consecutive image bytes, stem_rows_kernel); otherwise
+        # K = 147 (k = tap*3 + c) padded to 160
         w, t = _fold(p, "conv1.weight", "bn1")
-        self.stem_wp = pack_fragments(w, 4, 5, self.dtype).to(dev).contiguous()
+        self.stem_rows = self.in_kind == "u8" and os.environ.get("KDL_STEM_ROWS", "1") != "0"
+        if self.stem_rows:
+            self.stem_wp = pack_fragments(rowrun_weights(w, 7, 21, 32), 4, 7, self.dtype).to(dev).contiguous()
+        else:
+            self.stem_wp = pack_fragments(w, 4, 5, self.dtype).to(dev).contiguous()
         self.stem_bias = t.float().to(dev)
         oh = (S + 6 - 7) // 2 + 1                                   # 112
         self.steps.append(Step("stem", "conv1", src="input", dst="stem", geom=(S, S, oh, oh)))
@@ -163,7 +170,8 @@ class ResNetEngine(EngineBase):
                                           in_kind=0 if self.in_kind == "u8" else 1,
                                           KH=7, KW=7, stride=2, pad=3, cout=64, relu=1,
                                           scale0=sc[0], scale1=sc[1], scale2=sc[2],
-                                          shift0=sh[0], shift1=sh[1], shift2=sh[2], dt=self.dt))
+                                          shift0=sh[0], shift1=sh[1], shift2=sh[2], dt=self.dt,
+                                          rows=int(self.stem_rows)))
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=None, y=self._ptr(step.dst),
                                               B=b, H=H, W=W, OH=OH, OW=OW, C=step.extra["C"],

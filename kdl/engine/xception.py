@@ -28,7 +28,7 @@ from ..models.layers import tf_same_pad
 from ..ops import _lib
 from ..ops.conv import (MODE_CONV, MODE_DW, MODE_PW, ConvGemmLayer, Geometry,
                         conv_weights_nk)
-from ..ops.pack import bn_scale_shift, pack_fragments, round_up
+from ..ops.pack import bn_scale_shift, pack_fragments, round_up, rowrun_weights
 from .base import EngineBase, Step
 
 
@@ -74,7 +74,12 @@ class XceptionEngine(EngineBase):
         else:
             bias = t
         oh1 = (S - 3) // 2 + 1
-        self.stem_wp = pack_fragments(w, 2, 1).to(dev).contiguous()
+        # uint8 input: row-run K layout (k = ky*16 + kx*3 + c, 2 k-steps; stem_rows_kernel)
+        self.stem_rows = self.in_kind == "u8" and os.environ.get("KDL_STEM_ROWS", "1") != "0"
+        if self.stem_rows:
+            self.stem_wp = pack_fragments(rowrun_weights(w, 3, 9, 16), 2, 2).to(dev).contiguous()
+        else:
+            self.stem_wp = pack_fragments(w, 2, 1).to(dev).contiguous()
         self.stem_bias = bias.float().to(dev)
         self.steps.append(Step("stem", c1.name, src="input", dst="stem1", geom=(S, S, oh1, oh1)))
         self.shapes["stem1"] = (oh1, oh1, 32)
@@ -225,7 +230,7 @@ class XceptionEngine(EngineBase):
             prog.add_stem(step.name, dict(x=self.input_ptr(), wp=_lib.ptr(self.stem_wp),
                                           bias=_lib.ptr(self.stem_bias), y=self._ptr(step.dst),
                                           B=b, H=H, W=W, OH=OH, OW=OW, ldy=32,
-                                          in_kind=0 if self.in_kind == "u8" else 1))
+                                          in_kind=0 if self.in_kind == "u8" else 1, rows=int(self.stem_rows)))
         elif step.kind in ("conv", "convpool"):
             self._emit_conv(prog, step, b)
         elif step.kind == "pool":

@@ -45,3 +45,12 @@ def pad_vec(v: torch.Tensor, n: int) -> torch.Tensor:
     out = torch.zeros(n, dtype=torch.float32)
     out[: v.numel()] = v.float()
     return out
+
+
+def rowrun_weights(w_nk: torch.Tensor, kh: int, run: int, rp: int) -> torch.Tensor:
+    """Stem weights W[N][kh*run] (k = ky*run + kx*3 + c) -> W[N][kh*rp]: every kernel row's
+    run of kx*3 + c slots zero-padded to rp (the K layout of stem_rows_kernel, stem.hip)."""
+    n = w_nk.shape[0]
+    out = torch.zeros(n, kh, rp, dtype=w_nk.dtype)
+    out[:, :, :run] = w_nk.reshape(n, kh, run)
+    return out.reshape(n, kh * rp)
