@@ -171,6 +171,8 @@ PoolAddArgs pool_args(const py::dict& d) {
   a.x = P<const uint16_t>(d, "x"); a.res = P<const uint16_t>(d, "res"); a.y = P<uint16_t>(d, "y");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
   a.C = I(d, "C"); a.pad_top = I(d, "pad_top"); a.pad_left = I(d, "pad_left"); a.dt = I(d, "dt");
+  a.algo = d.contains("algo") ? I(d, "algo") : 0;
+  a.seg = d.contains("seg") ? I(d, "seg") : 0; a.rb = d.contains("rb") ? I(d, "rb") : 0;
   return a;
 }
 HeadArgs head_args(const py::dict& d) {
@@ -196,6 +198,7 @@ DwArgs dw_args(const py::dict& d) {
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.C = I(d, "C"); a.relu_in = I(d, "relu_in");
   a.cg = d.contains("cg") ? I(d, "cg") : 0; a.rb = d.contains("rb") ? I(d, "rb") : 0;
   a.tw = d.contains("tw") ? I(d, "tw") : 0; a.seg = d.contains("seg") ? I(d, "seg") : 0;
+  a.algo = d.contains("algo") ? I(d, "algo") : 0; a.pd = d.contains("pd") ? I(d, "pd") : 0;
   return a;
 }
 

@@ -1,6 +1,8 @@
 // Depthwise 3x3 'same' conv (+ optional ReLU on load), NHWC bf16 -> bf16.
 // SURVEY.md §2.5 K5. Used by the "split" lowering of SeparableConv2D (dw kernel
-// then the MODE_PW GEMM); the autotuner picks split vs fused per layer.
+// then the MODE_PW GEMM); the autotuner picks split vs fused per layer. Two kernels:
+// the LDS-tiled one below (algo 1) and the direct row-streaming one further down
+// (algo 2, the default since it measured faster on every Xception shape).
 //
 // Block tile = one image x RB output rows x TW output columns x CG 8-channel
 // chunks. The (RB+2) x (TW+2) input patch (halo included; zeros outside the
@@ -155,6 +157,162 @@ __global__ __launch_bounds__(256) void dw3x3_tile_kernel(DwArgs a, int CG, int R
   }
 }
 
+// ---------------------------------------------------------------- direct row-streaming variant
+// No LDS, no barrier. A thread owns one 4-channel chunk (8-byte loads) x SEG adjacent output
+// columns x an RB-row band, flat-mapped with the chunk fastest: the 64 lanes of a wave read
+// 512 contiguous bytes of one pixel row (consecutive chunks), not a CB x segment rectangle,
+// so any C % 4 == 0 coalesces (Xception's 736-channel middle flow included). The band's
+// input rows stream top to bottom, PD rows in flight ahead of the one being used; each row
+// is loaded once, ReLU'd on load, unpacked once and FMA'd (packed fp32) into the
+// accumulators of the up-to-3 output rows it feeds; an output row is stored as soon as its
+// last input row has passed. The loop is unrolled by 3 input rows so every accumulator slot
+// index is a compile-time constant. Workgroups are XCD-remapped so neighbouring bands (which
+// share 2 halo rows) run on one XCD's L2. What it replaces: the LDS-tiled kernel above
+// stages a patch, syncs, then computes, so one workgroup's loads never overlap its own
+// arithmetic (measured 1.8 TB/s on the 19x19x736 middle-flow shape).
+template <int SEG, int PD>
+__global__ __launch_bounds__(256) void dw3x3_direct_kernel(DwArgs a, int RB, int nseg, int nbands, int nwg) {
+  constexpr int NJ = SEG + 2;
+  const int C4 = a.C >> 2;
+  const long id = (long)xcd_remap(blockIdx.x, nwg) * 256 + threadIdx.x;
+  const long total = (long)a.B * nbands * nseg * C4;
+  if (id >= total) return;                       // no barrier anywhere below
+  const int chunk = (int)(id % C4);
+  long r = id / C4;
+  const int seg = (int)(r % nseg);
+  r /= nseg;
+  const int band = (int)(r % nbands);
+  const int b = (int)(r / nbands);
+  const int ch = chunk * 4;
+  const int w0 = seg * SEG, h0 = band * RB;
+  const int rows = min(RB, a.H - h0);
+  const int vmax = rows + 2;                     // input rows h0-1 .. h0+rows
+
+  f32x2 wt[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const float4 q = *(const float4*)(a.w + (long)t * a.C + ch);
+    wt[t][0] = (f32x2){q.x, q.y};
+    wt[t][1] = (f32x2){q.z, q.w};
+  }
+  f32x2 acc[3][SEG][2];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int o = 0; o < SEG; ++o) acc[s][o][0] = acc[s][o][1] = (f32x2){0.f, 0.f};
+
+  const long img = (long)b * a.H;
+  const uint16_t* xb = a.x + (img * a.W + (w0 - 1)) * a.C + ch;
+  uint16_t* yb = a.y + (img * a.W + w0) * a.C + ch;
+  bool cok[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cok[j] = (unsigned)(w0 - 1 + j) < (unsigned)a.W;
+  const bool relu = a.relu_in != 0;
+  auto load = [&](int v, u32x2 (&xr)[NJ]) {
+    const int ih = h0 - 1 + v;
+    const bool rok = v < vmax && (unsigned)ih < (unsigned)a.H;
+    const uint16_t* rp = xb + (long)ih * a.W * a.C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      xr[j] = (rok && cok[j]) ? *(const u32x2*)(rp + (long)j * a.C) : (u32x2){0u, 0u};
+  };
+  auto finish = [&](f32x2 (&ac)[SEG][2], int ol) {
+    uint16_t* rp = yb + (long)(h0 + ol) * a.W * a.C;
+#pragma unroll
+    for (int o = 0; o < SEG; ++o) {
+      if (w0 + o < a.W)
+        *(u32x2*)(rp + (long)o * a.C) = (u32x2){pack_bf16(ac[o][0][0], ac[o][0][1]),
+                                                pack_bf16(ac[o][1][0], ac[o][1][1])};
+      ac[o][0] = ac[o][1] = (f32x2){0.f, 0.f};
+    }
+  };
+
+  u32x2 xq[PD + 1][NJ];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) load(k, xq[k]);
+  for (int v0 = 0; v0 < vmax; v0 += 3) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int v = v0 + u;
+      if (v >= vmax) break;
+      load(v + PD, xq[PD]);
+      f32x2 xf[NJ][2];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        u32x2 d = xq[0][j];
+        if (relu) { d[0] = relu_bf16x2(d[0]); d[1] = relu_bf16x2(d[1]); }
+        xf[j][0] = (f32x2){bf_lo(d[0]), bf_hi(d[0])};
+        xf[j][1] = (f32x2){bf_lo(d[1]), bf_hi(d[1])};
+      }
+      // input row v feeds output row ol = v - dy with tap row dy
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const int ol = v - dy;
+        if (ol < 0 || ol >= rows) continue;
+        const int slot = (u - dy + 3) % 3;       // == ol % 3 (v0 is a multiple of 3)
+#pragma unroll
+        for (int o = 0; o < SEG; ++o)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              acc[slot][o][h] = __builtin_elementwise_fma(xf[o + dx][h], wt[dy * 3 + dx][h], acc[slot][o][h]);
+        if (dy == 2) finish(acc[slot], ol);
+      }
+#pragma unroll
+      for (int k = 0; k < PD; ++k)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) xq[k][j] = xq[k + 1][j];
+    }
+  }
+}
+
+// Direct-variant plan. The Xception shapes take (seg, rb, pd) from the batch-32 sweep of
+// tools/dwbench.py --direct on MI355X (profiles/dw_direct_sweep.txt; 1.3-1.9x the tiled
+// kernel on every shape); anything else gets SEG 3 and row bands sized for ~2 waves of
+// 256-thread workgroups per SIMD over the 256 CUs. a.rb / a.seg / a.pd override.
+struct DwdTile { short H, C, seg, rb, pd; };
+static const DwdTile kDwdTable[] = {
+    {147, 64, 3, 7, 1}, {147, 128, 4, 10, 2}, {74, 128, 3, 5, 1}, {74, 256, 3, 5, 1}, {37, 256, 3, 4, 1},
+    {37, 736, 2, 19, 1}, {19, 736, 4, 5, 2},  {10, 1024, 4, 2, 1}, {10, 1536, 2, 5, 2},
+};
+
+static void dwd_plan(const DwArgs& a, int* seg, int* rb, int* pd, int* nseg, int* nbands) {
+  const DwdTile* t = nullptr;
+  for (const DwdTile& e : kDwdTable)
+    if (e.H == a.H && e.H == a.W && e.C == a.C) t = &e;
+  *seg = a.seg > 0 ? a.seg : t ? t->seg : 3;
+  *nseg = (a.W + *seg - 1) / *seg;
+  const long per_band = (long)a.B * *nseg * (a.C / 4);
+  int R = a.rb > 0 ? a.rb : (t && a.seg <= 0) ? t->rb : 0;
+  if (R <= 0) {
+    long nb = (2L * 256 * 4 * 64 + per_band - 1) / per_band;
+    nb = nb < 1 ? 1 : (nb > a.H ? a.H : nb);
+    R = (int)((a.H + nb - 1) / nb);
+    if (R < 3 && a.H >= 3) R = 3;
+  }
+  *rb = R;
+  *nbands = (a.H + R - 1) / R;
+  *pd = a.pd > 0 ? a.pd : (t && a.seg <= 0 && a.rb <= 0) ? t->pd : 1;
+}
+
+static hipError_t dw3x3_direct(const DwArgs& a, hipStream_t s) {
+  int seg, rb, pd, nseg, nb;
+  dwd_plan(a, &seg, &rb, &pd, &nseg, &nb);
+  if (a.C % 4 != 0 || rb <= 0) return hipErrorInvalidValue;
+  const long total = (long)a.B * nb * nseg * (a.C / 4);
+  const long nblk = (total + 255) / 256;
+  if (nblk >= (1L << 31)) return hipErrorInvalidValue;
+  const int g = (int)nblk;
+#define KDL_DWD(sg, p) \
+  if (seg == sg && pd == p) { \
+    hipLaunchKernelGGL((dw3x3_direct_kernel<sg, p>), dim3(g), dim3(256), 0, s, a, rb, nseg, nb, g); \
+    return hipGetLastError(); }
+  KDL_DWD(2, 1) KDL_DWD(2, 2) KDL_DWD(3, 1) KDL_DWD(3, 2) KDL_DWD(4, 1) KDL_DWD(4, 2)
+#undef KDL_DWD
+  return hipErrorInvalidValue;
+}
+
 static size_t dw_smem(int CG, int RB, int TW) {
   return (size_t)9 * CG * 8 * 4 + (size_t)(RB + 2) * (TW + 2) * CG * 16;
 }
@@ -179,8 +337,17 @@ static void dw_pick(const DwArgs& a, int& CG, int& RB, int& TW, int& SEG) {
   }
 }
 
+// a.algo, else KDL_DW_ALGO (A/B runs), else the default below
+static int dw_algo(const DwArgs& a) {
+  if (a.algo > 0) return a.algo;
+  static const int env = [] { const char* e = getenv("KDL_DW_ALGO"); return e ? atoi(e) : 0; }();
+  if (env > 0) return env;
+  return 2;                                      // direct: faster on every measured shape
+}
+
 hipError_t dw3x3(const DwArgs& a, hipStream_t s) {
   if (a.C % 8 != 0 || a.W <= 0 || a.H <= 0 || a.B <= 0) return hipErrorInvalidValue;
+  if (dw_algo(a) == 2) return dw3x3_direct(a, s);
   int CG, RB, TW, SEG;
   dw_pick(a, CG, RB, TW, SEG);
   const size_t smem = dw_smem(CG, RB, TW);

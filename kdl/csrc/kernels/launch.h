@@ -83,6 +83,8 @@ struct DwArgs {
   int B, H, W, C;         // C = padded channel stride (multiple of 8)
   int relu_in;
   int cg, rb, tw, seg;    // tile overrides (0 = host heuristic): 8-ch chunks, rows, cols, cols/item
+  int algo;               // 0 = auto, 1 = LDS-tiled, 2 = direct row-streaming (rb / seg / pd apply)
+  int pd;                 // direct kernel: input rows prefetched ahead (0 = default)
 };
 hipError_t dw3x3(const DwArgs& a, hipStream_t s);
 
@@ -114,6 +116,8 @@ struct PoolAddArgs {
   int B, H, W, OH, OW, C; // C multiple of 8
   int pad_top, pad_left;
   int dt;                 // element type: 0 bf16, 1 fp16
+  int algo;               // 0 auto, 1 pixel-per-thread, 2 row-streaming (seg / rb apply)
+  int seg, rb;            // row-streaming: output columns per thread, output rows per band (0 = plan)
 };
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s);
 

@@ -56,8 +56,136 @@ __global__ __launch_bounds__(256) void pool_add_kernel(PoolAddArgs a) {
   *(u32x4*)(a.y + p * a.C + cc * 8) = o;
 }
 
+// Row-streaming variant (algo 2): a thread owns one 8-channel chunk x SEG adjacent output
+// columns x an RB-row output band, flat-mapped with the chunk fastest (a wave reads 1 KiB
+// of contiguous pixel-row bytes). The band's 2*RB+1 input rows stream top to bottom, one
+// row in flight ahead: each input row is loaded ONCE per thread (2*SEG+1 pixels), reduced
+// horizontally to SEG column maxima, and folded into the single running output row --
+// input row 2k+2 both finishes output row k (+ residual, store) and starts row k+1. The
+// one-pixel-per-thread kernel above re-reads every input pixel ~2.25x through L1/L2.
+template <int DT, int SEG>
+__global__ __launch_bounds__(256) void pool_add_rows_kernel(PoolAddArgs a, int RB, int nseg, int nbands) {
+  using E = Elt<DT>;
+  constexpr int NJ = 2 * SEG + 1;
+  const int C8 = a.C >> 3;
+  const long id = (long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long)a.B * nbands * nseg * C8) return;          // no barrier below
+  const int cc = (int)(id % C8);
+  long r = id / C8;
+  const int seg = (int)(r % nseg);
+  r /= nseg;
+  const int band = (int)(r % nbands);
+  const int b = (int)(r / nbands);
+  const int ow0 = seg * SEG, oh0 = band * RB;
+  const int rows = min(RB, a.OH - oh0);
+  const int iw0 = 2 * ow0 - a.pad_left, ih0 = 2 * oh0 - a.pad_top;
+  const int vmax = 2 * rows + 1;
+  const uint16_t* xb = a.x + ((long)b * a.H * a.W + iw0) * a.C + cc * 8;
+  const long obase = ((long)b * a.OH + oh0) * a.OW + ow0;
+  bool cok[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cok[j] = (unsigned)(iw0 + j) < (unsigned)a.W;
+  auto load = [&](int v, u32x4 (&xr)[NJ], bool& ok) {
+    const int ih = ih0 + v;
+    ok = v < vmax && (unsigned)ih < (unsigned)a.H;
+    const uint16_t* rp = xb + (long)ih * a.W * a.C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (ok && cok[j]) xr[j] = *(const u32x4*)(rp + (long)j * a.C);
+  };
+  float acc[SEG][8];
+  u32x4 xq[2][NJ];
+  bool okq[2];
+  load(0, xq[0], okq[0]);
+  for (int v = 0; v < vmax; ++v) {
+    load(v + 1, xq[1], okq[1]);
+    float hm[SEG][8];
+#pragma unroll
+    for (int o = 0; o < SEG; ++o)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) hm[o][d] = -INFINITY;
+    if (okq[0]) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (!cok[j]) continue;
+        float f[8];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) { f[2 * d] = E::lo(xq[0][j][d]); f[2 * d + 1] = E::hi(xq[0][j][d]); }
+        // input column j feeds output columns o with 2o <= j <= 2o + 2
+#pragma unroll
+        for (int o = 0; o < SEG; ++o)
+          if (j >= 2 * o && j <= 2 * o + 2) {
+#pragma unroll
+            for (int d = 0; d < 8; ++d) hm[o][d] = fmaxf(hm[o][d], f[d]);
+          }
+      }
+    }
+    const int k = v >> 1;
+    if ((v & 1) == 0 && k >= 1) {                // row 2k finishes output row k-1
+      const long p0 = obase + (long)(k - 1) * a.OW;
+#pragma unroll
+      for (int o = 0; o < SEG; ++o) {
+        if (ow0 + o >= a.OW) continue;
+        float m[8];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) m[d] = fmaxf(acc[o][d], hm[o][d]);
+        if (a.res) {
+          const u32x4 rr = *(const u32x4*)(a.res + (p0 + o) * a.C + cc * 8);
+#pragma unroll
+          for (int d = 0; d < 4; ++d) { m[2 * d] += E::lo(rr[d]); m[2 * d + 1] += E::hi(rr[d]); }
+        }
+        u32x4 out;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) out[d] = E::pack(m[2 * d], m[2 * d + 1]);
+        *(u32x4*)(a.y + (p0 + o) * a.C + cc * 8) = out;
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < SEG; ++o)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) acc[o][d] = (v & 1) ? fmaxf(acc[o][d], hm[o][d]) : hm[o][d];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) xq[0][j] = xq[1][j];
+    okq[0] = okq[1];
+  }
+}
+
+static void pool_rows_plan(const PoolAddArgs& a, int* seg, int* rb, int* nseg, int* nb) {
+  *seg = a.seg > 0 ? a.seg : 2;
+  *nseg = (a.OW + *seg - 1) / *seg;
+  const long per_band = (long)a.B * *nseg * (a.C / 8);
+  int R = a.rb;
+  if (R <= 0) {
+    long n = (2L * 256 * 4 * 64 + per_band - 1) / per_band;
+    n = n < 1 ? 1 : (n > a.OH ? a.OH : n);
+    R = (int)((a.OH + n - 1) / n);
+  }
+  *rb = R;
+  *nb = (a.OH + R - 1) / R;
+}
+
+static int pool_algo(const PoolAddArgs& a) {
+  if (a.algo > 0) return a.algo;
+  static const int env = [] { const char* e = getenv("KDL_POOL_ALGO"); return e ? atoi(e) : 0; }();
+  return env > 0 ? env : 1;
+}
+
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
   if (a.C % 8 != 0 || a.dt < 0 || a.dt > 1 || a.B <= 0 || a.OH <= 0 || a.OW <= 0) return hipErrorInvalidValue;
+  if (pool_algo(a) == 2) {
+    int seg, rb, nseg, nb;
+    pool_rows_plan(a, &seg, &rb, &nseg, &nb);
+    const long nblk = ((long)a.B * nb * nseg * (a.C / 8) + 255) / 256;
+    if (rb <= 0 || nblk >= (1L << 31)) return hipErrorInvalidValue;
+#define KDL_POOLR(et, sg)                                                                                    \
+    if (a.dt == et && seg == sg) {                                                                            \
+      hipLaunchKernelGGL((pool_add_rows_kernel<et, sg>), dim3((unsigned)nblk), dim3(256), 0, s, a, rb, nseg, nb); \
+      return hipGetLastError();                                                                               \
+    }
+    KDL_POOLR(0, 1) KDL_POOLR(0, 2) KDL_POOLR(0, 4) KDL_POOLR(1, 1) KDL_POOLR(1, 2) KDL_POOLR(1, 4)
+#undef KDL_POOLR
+    return hipErrorInvalidValue;
+  }
   if ((long)a.B * a.OH > 65535) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((a.OW * (a.C / 8) + 255) / 256), (unsigned)(a.B * a.OH));
   if (a.dt) hipLaunchKernelGGL(pool_add_kernel<1>, grid, dim3(256), 0, s, a);

@@ -110,6 +110,32 @@ def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
             raise AssertionError(f"split={split} cfg={cfg}: {e}") from None
 
 
+@pytest.mark.parametrize("H,C,relu", [(19, 736, True), (37, 256, True), (74, 128, False), (10, 1024, False),
+                                      (23, 96, True)])
+def test_dw3x3_tiled_and_direct(H, C, relu):
+    """Standalone depthwise 3x3 'same' (split separable lowering): LDS-tiled kernel (algo 1)
+    and the direct row-streaming kernel (algo 2, several seg / band / prefetch shapes incl.
+    partial bands and partial column segments) against torch fp32."""
+    import torch.nn.functional as F
+    C_ = _lib.lib()
+    gen = torch.Generator().manual_seed(11)
+    B = 3
+    x = torch.randn(B, H, H, C, generator=gen).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(9, C, generator=gen) / 3).float().to(DEV).contiguous()
+    xf = x.float().permute(0, 3, 1, 2)
+    xf = xf.relu() if relu else xf
+    ref = F.conv2d(F.pad(xf, (1, 1, 1, 1)), w.t().reshape(C, 1, 3, 3), groups=C).permute(0, 2, 3, 1)
+    base = dict(x=x.data_ptr(), w=w.data_ptr(), B=B, H=H, W=H, C=C, relu_in=int(relu))
+    s = torch.cuda.current_stream().cuda_stream
+    for kw in [dict(algo=1), dict(algo=2), dict(algo=2, seg=2, rb=2, pd=2), dict(algo=2, seg=3, rb=5, pd=1),
+               dict(algo=2, seg=4, rb=H, pd=2)]:
+        y = torch.full_like(x, float("nan"))
+        C_.dw3x3({**base, "y": y.data_ptr(), **kw}, s)
+        torch.cuda.synchronize()
+        err = (y.float() - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item(), (kw, err)
+
+
 def test_sepconv_2d_repeat_race_screen():
     """2-D tiled fused separable conv: run-to-run identical on an early-flow shape."""
     gen = torch.Generator().manual_seed(5)
@@ -189,6 +215,15 @@ def test_pool_add(H, C, with_res):
     ref = pool_add_ref(x, res, B, H, H, OH, OH, C, pt)
     err = (y.float().view(-1, C) - ref).abs().max().item()
     assert err <= 2e-2 * ref.abs().max().item(), err
+    # both kernels explicitly: pixel-per-thread and row-streaming (partial bands / segments)
+    for kw in [dict(algo=1), dict(algo=2), dict(algo=2, seg=1, rb=1), dict(algo=2, seg=4, rb=3),
+               dict(algo=2, seg=2, rb=OH)]:
+        y.fill_(float("nan"))
+        _lib.lib().pool_add(dict(x=_lib.ptr(x), res=_lib.ptr(res), y=_lib.ptr(y), B=B, H=H, W=H, OH=OH, OW=OH,
+                                 C=C, pad_top=pt, pad_left=pt, **kw), _lib.stream_ptr())
+        torch.cuda.synchronize()
+        err = (y.float().view(-1, C) - ref).abs().max().item()
+        assert err <= 2e-2 * ref.abs().max().item(), (kw, err)
 
 
 @pytest.mark.parametrize("H,cin,C", [(147, 64, 128), (74, 128, 256), (37, 256, 736), (19, 736, 1024)])

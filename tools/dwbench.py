@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--direct", action="store_true",
+                    help="also time + check the direct row-streaming kernel (algo 2) over (seg, rb, pd)")
     a = ap.parse_args()
     C_ = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -65,6 +67,24 @@ def main():
         print(f"{name:6s} B{B} {H}x{W}x{C}: auto {t:7.1f} us  {gb / t * 1e6 / 1e3:5.2f} TB/s  err {err:.2e}",
               flush=True)
         assert err < 1e-2, err
+        if a.direct:
+            res = []
+            for seg in (2, 3, 4):
+                for rb in (0, 2, 3, 4, 5, 7, 10, 19, 37):
+                    for pd in (1, 2):
+                        if rb > H:
+                            continue
+                        kw = dict(algo=2, seg=seg, rb=rb, pd=pd)
+                        y.zero_()
+                        run(**kw)
+                        e2 = ((y.float() - r).abs().max() / r.abs().max()).item()
+                        assert e2 < 1e-2, (kw, e2)
+                        res.append((tm(**kw), kw))
+            res.sort(key=lambda q: q[0])
+            d0 = [q for q in res if q[1]["rb"] == 0 and q[1]["pd"] == 1]
+            print(f"    direct default-rb: " + "  ".join(f"seg{q[1]['seg']} {q[0]:.1f}" for q in d0), flush=True)
+            for q in res[:4]:
+                print(f"    direct {q[0]:7.1f} us {gb / q[0] * 1e3:5.2f} TB/s  {q[1]}", flush=True)
         if not a.sweep:
             continue
         C8 = C // 8
