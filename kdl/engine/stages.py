@@ -27,6 +27,7 @@ The reference has no equivalent (TF-Serving runs one session per batch).
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -146,12 +147,15 @@ def plan_stages(steps, split_after, scratch=()) -> StagePlan:
 class StagePipe:
     pipelined = True          # consecutive batches overlap (graph_tune times it free-running)
 
-    def __init__(self, engine, split_after, cu_share: list | None = None):
+    def __init__(self, engine, split_after, cu_share: list | None = None, priorities: list | None = None):
         """``split_after``: one step name (two stages) or a comma-separated list / list of
         names (one stage per segment, one HIP stream each). ``cu_share``: optional
         fraction of the CUs per stage (CU-masked streams, hipExtStreamCreateWithCUMask),
         so the stages run on disjoint CU sets; measured 20-65 % SLOWER than letting both
-        stages share every CU (profiles/stages_ab.txt), kept for experiments only."""
+        stages share every CU (profiles/stages_ab.txt), kept for experiments only.
+        ``priorities``: optional HIP stream priority per stage (lower = higher; env
+        ``KDL_STAGE_PRIO``, e.g. "0,-1"), so the hardware dispatcher places one stage's
+        workgroups first when both stages wait for free CUs."""
         self.engine = engine
         self.device = engine.device
         self.max_batch = engine.max_batch
@@ -167,7 +171,15 @@ class StagePipe:
             self.streams = [cu_masked_stream(self.device, _cu_mask(k, cu_share)) for k in range(K)]
             engine.stream = self.streams[0]
         else:
-            self.streams = [engine.stream] + [torch.cuda.Stream(device=self.device) for _ in range(K - 1)]
+            if priorities is None and os.environ.get("KDL_STAGE_PRIO"):
+                priorities = [int(v) for v in os.environ["KDL_STAGE_PRIO"].split(",")]
+            if priorities:
+                assert len(priorities) == K, (priorities, K)
+                self.streams = [torch.cuda.Stream(device=self.device, priority=p) for p in priorities]
+                engine.stream = self.streams[0]
+            else:
+                self.streams = [engine.stream] + [torch.cuda.Stream(device=self.device) for _ in range(K - 1)]
+        self.priorities = priorities
         self.stream = self.streams[0]
         self.done = [[torch.cuda.Event() for _ in range(K)] for _ in range(2)]   # [parity][stage]
         self._fork = torch.cuda.Event()
