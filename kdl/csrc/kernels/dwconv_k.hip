@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
   const int cl = tid % CB, sl = tid / CB;
   const int ch = (cbk * CB + cl) * 4;
   const int seg = sb * SL + sl;
-  const bool live = seg < nseg;
+  const bool live = sl < SL && seg < nseg;     // CB not dividing 256: the last 256 % CB lanes idle
   const int w0 = seg * SEG;
   const int h0 = band * RB;
   const int rows = min(RB, a.OH - h0);
@@ -428,12 +428,22 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
 
 // Direct-variant plan: CB = widest chunk block dividing C/4; SEG 2 for 5x5, 4 for 3x3;
 // row bands sized for >= 64 workgroups per image (the engine sizes the SE partials per
-// image, so the plan must not depend on the batch).
+// image, so the plan must not depend on the batch). When only a 8/16-chunk block divides
+// C/4 (64/128 contiguous bytes per pixel: half-used cache lines, e.g. B7's 288 / 960 / 192
+// channels), a wider non-power-of-two block (24..48 chunks, the last 256 % CB lanes idle)
+// is taken instead (KDL_DWV_WIDE=0 restores the power-of-two rule).
 static void dwv_plan(const DwkArgs& a, int* cb, int* rb, int* seg, int* ntiles) {
   const int C4 = a.C / 4;
   *cb = 0;
   for (int c : {64, 32, 16, 8})
     if (C4 % c == 0) { *cb = c; break; }
+  static const bool wide = [] { const char* e = getenv("KDL_DWV_WIDE"); return !e || atoi(e) != 0; }();
+  // measured (profiles/dwv_wide_ab.txt): 150x150x288 s1 -13 %, 38x38x960 s1 -15 %, 75x75x480 s2
+  // -6 %, but 300x300x192 s2 (16 -> 48 chunks) +5 %: a 16-chunk block is widened at stride 1 only
+  if (wide && (*cb == 8 || (*cb == 16 && a.S == 1)) && a.cg <= 0)
+    for (int c : {48, 40, 36, 24})
+      if (C4 % c == 0) { *cb = c; break; }
+  if (a.cg > 0 && C4 % a.cg == 0) *cb = a.cg;  // explicit chunk block (sweeps)
   const DwkTile* t = dwk_lookup(a);
   const bool tab = t != nullptr && t->algo == 2;
   *seg = a.seg > 0 ? a.seg : tab ? t->seg : (a.K == 5 ? 2 : 4);
@@ -504,7 +514,8 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
     return hipGetLastError();                                                                         \
   }
 #define KDL_DWV(k, st, sg, cb) KDL_DWV1(k, st, sg, cb, 1) KDL_DWV1(k, st, sg, cb, 3)
-#define KDL_DWV_CB(k, st, sg) KDL_DWV(k, st, sg, 8) KDL_DWV(k, st, sg, 16) KDL_DWV(k, st, sg, 32) KDL_DWV(k, st, sg, 64)
+#define KDL_DWV_CB(k, st, sg) KDL_DWV(k, st, sg, 8) KDL_DWV(k, st, sg, 16) KDL_DWV(k, st, sg, 32) KDL_DWV(k, st, sg, 64) \
+  KDL_DWV(k, st, sg, 24) KDL_DWV(k, st, sg, 36) KDL_DWV(k, st, sg, 40) KDL_DWV(k, st, sg, 48)
 #define KDL_DWV_KS(k, st) KDL_DWV_CB(k, st, 2) KDL_DWV_CB(k, st, 4)
   KDL_DWV_KS(3, 1) KDL_DWV_KS(3, 2) KDL_DWV_KS(5, 1) KDL_DWV_KS(5, 2)
 #undef KDL_DWV_KS
