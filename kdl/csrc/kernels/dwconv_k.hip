@@ -205,12 +205,14 @@ static size_t dwk_smem(int K, int S, int CG, int RB, int TW) {
 // 25 % slower summed over B7) -- keep the CG with the tallest band, ties -> wider CG.
 // SEG odd: the items of a wave then start on different LDS bank slots (stride 2: with the
 // patch column-deinterleaved). a.cg/rb/tw/seg override everything.
+// 5x5 stride-1 rows at 75x75x480 / 38x38x960 / 38x38x1344 moved to the direct kernel once it took wide
+// chunk blocks (profiles/dwv_wide_ab.txt: 203 -> 170, 90 -> 86, 127 -> 106 us)
 struct DwkTile { short H, W, C, K, S, algo, cg, rb, tw, seg; };   // algo 2: rb / seg of dwv_kernel, tw = prefetch rows
 static const DwkTile kDwkTable[] = {
     {300, 300, 64, 3, 1, 2, 0, 16, 0, 4},   {300, 300, 32, 3, 1, 2, 0, 16, 0, 2},  {300, 300, 192, 3, 2, 2, 0, 6, 0, 2},
-    {150, 150, 288, 3, 1, 2, 0, 38, 0, 2},  {150, 150, 288, 5, 2, 2, 0, 16, 0, 4}, {75, 75, 480, 5, 1, 1, 4, 8, 38, 5},
-    {75, 75, 480, 3, 2, 2, 0, 38, 0, 2},    {38, 38, 960, 3, 1, 2, 0, 8, 0, 4},    {38, 38, 960, 5, 1, 1, 4, 8, 38, 5},
-    {38, 38, 1344, 5, 1, 1, 4, 8, 38, 5},   {38, 38, 1344, 5, 2, 2, 0, 12, 0, 2},  {19, 19, 2304, 5, 1, 1, 8, 12, 19, 5},
+    {150, 150, 288, 3, 1, 2, 0, 38, 0, 2},  {150, 150, 288, 5, 2, 2, 0, 16, 0, 4}, {75, 75, 480, 5, 1, 2, 0, 38, 3, 2},
+    {75, 75, 480, 3, 2, 2, 0, 38, 0, 2},    {38, 38, 960, 3, 1, 2, 0, 8, 0, 4},    {38, 38, 960, 5, 1, 2, 0, 38, 3, 2},
+    {38, 38, 1344, 5, 1, 2, 0, 38, 1, 2},   {38, 38, 1344, 5, 2, 2, 0, 12, 0, 2},  {19, 19, 2304, 5, 1, 1, 8, 12, 19, 5},
     {19, 19, 2304, 3, 1, 1, 8, 8, 19, 5},   {19, 19, 3840, 3, 1, 1, 8, 12, 19, 5},
 };
 

@@ -1,0 +1,13 @@
+#!/bin/bash
+# verify HEAD: full GPU suite, smoke, every family's default bench line
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+tools/gpu_session.sh \
+  t_all 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -- \
+  smoke 200 python -c "import __graft_entry__ as g; g.smoke()" -- \
+  v_xc 200 python bench.py -- \
+  v_xc_d 200 python bench.py --steps 20 --warmup 5 -- \
+  v_r50 200 python bench.py --model resnet50 --steps 100 --warmup 20 -- \
+  v_vit 200 python bench.py --model vit_b16 --steps 100 --warmup 20 -- \
+  v_vit8 200 python bench.py --model vit_b16_fp8 --steps 100 --warmup 20 -- \
+  v_eff 300 python bench.py --model efficientnet_b7 --steps 20 --warmup 5
