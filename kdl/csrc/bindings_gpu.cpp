@@ -44,6 +44,7 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.px = P<const uint16_t>(d, "px");
   a.pH = I(d, "pH"); a.pW = I(d, "pW"); a.pld = I(d, "pld"); a.ppad = I(d, "ppad");
   a.wimg = I(d, "wimg");
+  a.krot = I(d, "krot");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {

@@ -96,16 +96,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   // Issue stage t (k32 steps t*KSUB .. t*KSUB+KSUB-1). A sub-step past the end
   // of K re-issues the stage's first sub-step into its own slot (its MFMAs are
   // skipped), so every stage has exactly L*KSUB DMAs for the counted vmcnt.
-  const int krot = (ABL & 128) ? (int)(blockIdx.x % (unsigned)KT32) : 0;
+  const int krot = (ABL & 128) ? (int)(blockIdx.x % (unsigned)KT32) : a.krot ? (mi * 7) % KT32 : 0;
   auto issue = [&](int t, int buf) {
 #pragma unroll
     for (int ks = 0; ks < KSUB; ++ks) {
       int k32 = t * KSUB + ks;
       if (k32 >= KT32) k32 = t * KSUB;
-      if constexpr ((ABL & 128) != 0) {
-        k32 += krot;
-        k32 = k32 >= KT32 ? k32 - KT32 : k32;
-      }
+      k32 += krot;                            // uniform: rotated k order (0 = in order)
+      k32 = k32 >= KT32 ? k32 - KT32 : k32;
       long koff_a;
       if constexpr (MODE == 0) {
         koff_a = (long)k32 * 32;
@@ -299,8 +297,11 @@ static hipError_t launch_pipe_ablation(int cfg, const ConvGemmArgs& a, hipStream
   }
 }
 
-hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
-  if (a.K % 32 != 0 || a.M <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& args, hipStream_t s) {
+  if (args.K % 32 != 0 || args.M <= 0 || args.dt < 0 || args.dt > 1) return hipErrorInvalidValue;
+  static const int env_krot = [] { const char* e = getenv("KDL_PIPE_KROT"); return e ? atoi(e) : -1; }();
+  ConvGemmArgs a = args;
+  if (env_krot >= 0) a.krot = env_krot;
   if (cfg >= 27) return mode == 0 && a.dt == 0 ? launch_pipe_ablation(cfg, a, s) : hipErrorInvalidValue;
   if (mode == 0) return a.dt ? launch_pipe_mode<0, 1>(cfg, a, s) : launch_pipe_mode<0, 0>(cfg, a, s);
   if (mode == 1) return a.dt ? launch_pipe_mode<1, 1>(cfg, a, s) : launch_pipe_mode<1, 0>(cfg, a, s);

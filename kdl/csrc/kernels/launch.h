@@ -43,6 +43,10 @@ struct ConvGemmArgs {
   // only): wp points at [B][NF][K/32][64][8] and wimg is the element stride between images;
   // M tiles then never straddle two images. 0 = one weight set for every row.
   int wimg;
+  // LDS-DMA pipelined GEMM (gemm_pipe): 1 = every M tile walks K from its own starting
+  // step ((7*mi) mod K/32), so the workgroups sharing the weights do not all fetch the same
+  // fragments at launch (env KDL_PIPE_KROT overrides; 0 = in order)
+  int krot;
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
