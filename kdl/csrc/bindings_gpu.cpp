@@ -157,6 +157,7 @@ GemmF8Args f8_args(const py::dict& d) {
   a.y = P<uint16_t>(d, "y"); a.y8 = P<uint8_t>(d, "y8"); a.out_inv_scale = F(d, "out_inv_scale", 1.f);
   a.M = I(d, "M"); a.K = I(d, "K"); a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
   a.NF = I(d, "NF"); a.nstore = I(d, "nstore"); a.relu_out = I(d, "relu_out");
+  a.krot = I(d, "krot");
   return a;
 }
 FcMfmaArgs fcm_args(const py::dict& d) {

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
   const int mi = wg / nN, ni = wg % nN;
   const int m0 = mi * BM, n0 = ni * BN;
   const int KT = a.K >> 7;
+  const int krot = a.krot ? (mi * 7) % KT : 0;  // rotated k order: M tiles do not all fetch the same B at once
 
   long src[L];
   bool isa[L];
@@ -67,6 +68,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
   }
   auto issue = [&](int t, int buf) {
     uint8_t* base = smem + buf * STAGE;
+    t += krot;
+    t = t >= KT ? t - KT : t;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       const int hf = min(wave + i * NW, HF - 1);
@@ -179,7 +182,10 @@ int gemm_f8_config(int cfg, int* bm, int* bn, int* threads) {
   }
 }
 
-hipError_t gemm_f8(int cfg, const GemmF8Args& a, hipStream_t s) {
+hipError_t gemm_f8(int cfg, const GemmF8Args& args, hipStream_t s) {
+  static const int env_krot = [] { const char* e = getenv("KDL_F8_KROT"); return e ? atoi(e) : -1; }();
+  GemmF8Args a = args;
+  if (env_krot >= 0) a.krot = env_krot;
   int bm, bn, th;
   if (gemm_f8_config(cfg, &bm, &bn, &th) != 0 || a.K % 128 != 0 || a.ldx % 16 != 0 || (a.NF * 16) % bn != 0 ||
       a.M <= 0)

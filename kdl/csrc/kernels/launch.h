@@ -282,6 +282,7 @@ struct GemmF8Args {
   uint8_t* y8;            // e4m3 out [M][ldy], value / out_scale
   float out_inv_scale;
   int M, K, ldx, ldy, ldr, NF, nstore, relu_out;
+  int krot;               // 1: each M tile starts its K loop at its own 128-deep step (env KDL_F8_KROT overrides)
 };
 hipError_t gemm_f8(int cfg, const GemmF8Args& a, hipStream_t s);
 int gemm_f8_config(int cfg, int* bm, int* bn, int* threads);

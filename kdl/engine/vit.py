@@ -64,8 +64,10 @@ class ViTEngine(EngineBase):
             self.load_tuning(tune_file)
 
     def _lin(self, name: str, w: torch.Tensor, b: torch.Tensor, relu_out: int = 0) -> ConvGemmLayer:
-        return ConvGemmLayer(name, MODE_PW, w.double(), b.float(), cin_pad=w.shape[1], n=w.shape[0],
-                             relu_out=relu_out, device=self.device)
+        lay = ConvGemmLayer(name, MODE_PW, w.double(), b.float(), cin_pad=w.shape[1], n=w.shape[0],
+                            relu_out=relu_out, device=self.device)
+        lay.krot = 1    # K-rotated LDS-DMA GEMM: bf16 +0.6 % img/s, p50 -2.9 % (profiles/krot_ab.txt)
+        return lay
 
     def _build(self, p: dict) -> None:
         dev, D = self.device, V.DIM
