@@ -84,7 +84,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   // tile share it, so their band reads stay L2-shared): without it all workgroups fetch the
   // same weight fragments at the same time
   int krot = 0;
-  if constexpr ((ABL & 32) != 0) krot = (mi * 7) % KT;
+  if constexpr ((ABL & 32) != 0) krot = (mi * (a.krot > 0 ? a.krot : 7)) % KT;   // a.krot: multiplier (probes)
   auto kc = [&](int t) {
     t = min(t, KT - 1) + krot;
     return t >= KT ? t - KT : t;
@@ -407,7 +407,11 @@ int sepconv_ws_fits(int cfg, int W) {
   }
 }
 
-hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s) {
+hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
+  // KDL_WS_KMUL: K-rotation multiplier of the rotated ids (default 7; A/B probes only)
+  static const int env_kmul = [] { const char* e = getenv("KDL_WS_KMUL"); return e ? atoi(e) : 0; }();
+  ConvGemmArgs a = args;
+  if (env_kmul > 0) a.krot = env_kmul;
   int bm, bn, th;
   // ids 9 / 10 (ablation bit 2, no pointwise MFMA) faulted the GPU once in round 2 (cause not
   // found); refused until understood -- they are timing ablations, never candidates
