@@ -150,16 +150,16 @@ PYBIND11_MODULE(_rt, m) {
         py::gil_scoped_release nogil;
         return b.wait(ticket, p, cap);
       })
-      .def("next_batch", [](DynamicBatcher& b, uintptr_t staging, int64_t poll_us) -> py::object {
+      .def("next_batch", [](DynamicBatcher& b, uintptr_t staging, int64_t poll_us, bool eager) -> py::object {
         Batch batch;
         bool ok;
         {
           py::gil_scoped_release nogil;
-          ok = b.next_batch(reinterpret_cast<uint8_t*>(staging), poll_us, &batch);
+          ok = b.next_batch(reinterpret_cast<uint8_t*>(staging), poll_us, &batch, eager);
         }
         if (!ok) return py::none();
         return py::cast(batch);
-      })
+      }, py::arg("staging"), py::arg("poll_us"), py::arg("eager") = false)
       .def("finish", [](DynamicBatcher& b, const Batch& batch, uintptr_t results, int status) {
         py::gil_scoped_release nogil;
         b.finish(batch, reinterpret_cast<const float*>(results), status);

@@ -91,7 +91,7 @@ int DynamicBatcher::wait(int64_t ticket, float* out, size_t out_floats) {
   return status;
 }
 
-bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b) {
+bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, bool eager) {
   std::vector<std::shared_ptr<Req>> take;
   {
     std::unique_lock<std::mutex> lk(mu_);
@@ -115,7 +115,7 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b) {
       if (!queue_.empty()) {
         const bool full = queued_items_ >= opt_.max_batch_size;
         const bool timed_out = now - queue_.front()->enqueue_us >= opt_.batch_timeout_us;
-        if (full || timed_out) break;
+        if (full || timed_out || eager) break;
         const int64_t wake = std::min(give_up, queue_.front()->enqueue_us + opt_.batch_timeout_us);
         if (now >= give_up) return false;
         cv_consumer_.wait_for(lk, std::chrono::microseconds(std::max<int64_t>(1, wake - now)));

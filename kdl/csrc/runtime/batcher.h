@@ -67,8 +67,11 @@ class DynamicBatcher {
   // buffer is not written and the call returns ST_ERROR). Returns a BatchStatus.
   int wait(int64_t ticket, float* out, size_t out_floats);
 
-  // Consumer: waits up to poll_us for a batch; false on timeout/shutdown.
-  bool next_batch(uint8_t* staging, int64_t poll_us, Batch* b);
+  // Consumer: waits up to poll_us for a batch; false on timeout/shutdown. A batch forms
+  // when max_batch_size items are queued or the oldest has waited batch_timeout_us; with
+  // `eager` (the caller's device is idle) as soon as anything is queued -- work-conserving
+  // dispatch: an idle GPU never waits out the timeout, a busy one still gets full batches.
+  bool next_batch(uint8_t* staging, int64_t poll_us, Batch* b, bool eager = false);
   void finish(const Batch& b, const float* results, int status);
 
   void shutdown();

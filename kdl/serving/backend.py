@@ -187,6 +187,8 @@ class _Executor(threading.Thread):
         self.healthy = True
         self.failures = 0
         self.faults = runner.faults
+        bp = runner.cfg.batching
+        self.eager = bool(runner.cfg.enable_batching and getattr(bp, "eager_when_idle", True))
 
     def run(self):
         try:
@@ -209,7 +211,9 @@ class _Executor(threading.Thread):
         slot = 0
         while not self.stop.is_set():
             poll = 0 if pending else 100_000   # with work in flight, never sleep in the batcher
-            batch = b.next_batch(self.staging_ptr(slot), poll)
+            # device idle: dispatch what is queued now (work-conserving) instead of waiting
+            # out the batch timeout; device busy: only full (or timed-out) batches
+            batch = b.next_batch(self.staging_ptr(slot), poll, self.eager and not pending)
             if batch is not None:
                 t0 = time.perf_counter()
                 METRICS.observe("kdl_stage_ms", (rt.now_us() - batch.oldest_enqueue_us) / 1e3, stage="queue_wait")

@@ -22,6 +22,9 @@ class BatchingParams:
     max_enqueued_batches: int = 1000
     num_batch_threads: int = 1
     allowed_batch_sizes: list[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 32])
+    # kdl extension (not a TF-Serving knob): an executor whose device is idle takes whatever is
+    # queued at once instead of waiting out batch_timeout_micros (work-conserving dispatch)
+    eager_when_idle: bool = True
 
     @classmethod
     def parse(cls, text: str) -> "BatchingParams":
@@ -86,6 +89,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--executors_per_gpu", type=int, default=1)
     ap.add_argument("--max_batch_size", type=int, default=None)
     ap.add_argument("--batch_timeout_micros", type=int, default=None)
+    ap.add_argument("--eager_dispatch", default="true",
+                    help="an idle executor takes whatever is queued at once instead of waiting out "
+                         "batch_timeout_micros (kdl extension; 'false' = TF-Serving behaviour)")
     ap.add_argument("--allowed_batch_sizes", default=None, help="comma separated, e.g. 1,4,8,16,32")
     ap.add_argument("--synthetic_model", action="store_true")
     ap.add_argument("--host", default="0.0.0.0")
@@ -119,6 +125,7 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
         bp.allowed_batch_sizes = [b for b in bp.allowed_batch_sizes if b < a.max_batch_size] + [a.max_batch_size]
     if a.batch_timeout_micros is not None:
         bp.batch_timeout_micros = a.batch_timeout_micros
+    bp.eager_when_idle = _truthy(a.eager_dispatch)
     if a.allowed_batch_sizes:
         bp.allowed_batch_sizes = sorted(int(x) for x in a.allowed_batch_sizes.split(","))
         bp.max_batch_size = bp.allowed_batch_sizes[-1]

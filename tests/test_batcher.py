@@ -75,6 +75,23 @@ def test_timeout_flushes_partial_batch_into_bucket():
     assert b.bucket_for(5) == 8 and b.bucket_for(1) == 1
 
 
+def test_eager_dispatch_skips_the_timeout_when_idle():
+    """eager next_batch (the executor's device is idle) returns a partial batch at once;
+    the non-eager call waits the batch timeout out first."""
+    b = _mk(timeout_us=500_000)
+    data = np.full(3 * ITEM, 7, np.uint8)
+    staging = np.zeros(8 * ITEM, np.uint8)
+    t = b.submit(data, 3, 0)
+    t0 = time.perf_counter()
+    assert b.next_batch(staging.ctypes.data, 0) is None          # not full, not timed out
+    batch = b.next_batch(staging.ctypes.data, 0, True)
+    assert time.perf_counter() - t0 < 0.25
+    assert batch is not None and batch.n_real == 3 and batch.bucket == 4
+    assert (staging[:3 * ITEM] == 7).all()
+    b.finish(batch, np.zeros((4, 2), np.float32).ctypes.data, rt.ST_OK)
+    assert b.wait(t, np.zeros((3, 2), np.float32)) == rt.ST_OK
+
+
 def test_deadline_expires_queued_request():
     b = _mk(timeout_us=10_000_000)          # never flushes by timeout
     data = np.zeros(ITEM, np.uint8)

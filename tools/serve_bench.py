@@ -58,6 +58,9 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--max-batch", type=int, default=32)
     ap.add_argument("--timeout-us", type=int, default=1000)
+    ap.add_argument("--no-eager", action="store_true",
+                    help="idle executors wait out the batch timeout (TF-Serving behaviour) instead of "
+                         "dispatching whatever is queued")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--client-procs", type=int, default=0,
                     help="run the clients in this many spawned processes (0: threads of the server "
@@ -97,7 +100,7 @@ def main(argv=None) -> int:
         cfg = ServerConfig(port=0, rest_api_port=0, model_base_path=base, device=a.device, gpus=a.gpus,
                            host="127.0.0.1", file_system_poll_wait_seconds=0, grpc_max_threads=max(64, a.clients * 2),
                            batching=BatchingParams(max_batch_size=a.max_batch, batch_timeout_micros=a.timeout_us,
-                                                   allowed_batch_sizes=sizes))
+                                                   allowed_batch_sizes=sizes, eager_when_idle=not a.no_eager))
         srv = ModelServer(cfg).start(block_until_loaded=True)
         if a.signature != "serving_default":
             srv.manager.get("clothing-model").runner(a.signature)
