@@ -67,6 +67,31 @@ def test_conv_gemm_pointwise(cin, n, H, stride):
         _check(y, ref, n)
 
 
+@pytest.mark.parametrize("mode,cin,n,H", [(MODE_PW, 736, 736, 19), (MODE_PW, 768, 3072, 14), (MODE_CONV, 64, 64, 30)])
+def test_gemm_pipe_k_rotation(mode, cin, n, H):
+    """K-rotated LDS-DMA GEMM (ConvGemmArgs.krot: each M tile starts its K loop at its own
+    step) against the fp32 reference on every pipelined config, incl. KSUB > 1 tails."""
+    from kdl.ops.conv import PIPE_BASE, SEP_BASE
+    gen = torch.Generator().manual_seed(12)
+    lay = _layer(mode, cin, n, gen, relu_out=True)
+    lay.krot = 1
+    B = 3
+    OH = H - 2 if mode == MODE_CONV else H
+    g = Geometry(B, H, H, OH, OH)
+    x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
+    ref = conv_gemm_ref(lay, x, g)
+    cfgs = [c for _, c in lay.variants(H) if PIPE_BASE <= c < SEP_BASE]
+    assert cfgs
+    for cfg in cfgs:
+        y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
+        lay.launch(x, y, g, cfg=cfg)
+        torch.cuda.synchronize()
+        try:
+            _check(y, ref, n)
+        except AssertionError as e:
+            raise AssertionError(f"cfg={cfg}: {e}") from None
+
+
 def test_conv_gemm_conv3x3():
     gen = torch.Generator().manual_seed(2)
     lay = _layer(MODE_CONV, 32, 64, gen, relu_out=True)
