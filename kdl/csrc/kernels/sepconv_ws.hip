@@ -84,7 +84,11 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   // tile share it, so their band reads stay L2-shared): without it all workgroups fetch the
   // same weight fragments at the same time
   int krot = 0;
-  if constexpr ((ABL & 32) != 0) krot = (mi * (a.krot > 0 ? a.krot : 7)) % KT;   // a.krot: multiplier (probes)
+  if constexpr ((ABL & 32) != 0) {
+    // a.krot: multiplier (probes); a.wimg (unused by ws) < 0: the N tiles of an M tile also
+    // start half a K loop apart (KDL_WS_NROT probe)
+    krot = (mi * (a.krot > 0 ? a.krot : 7) + (a.wimg < 0 ? ni * (KT / 2) : 0)) % KT;
+  }
   auto kc = [&](int t) {
     t = min(t, KT - 1) + krot;
     return t >= KT ? t - KT : t;
@@ -412,6 +416,8 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
   static const int env_kmul = [] { const char* e = getenv("KDL_WS_KMUL"); return e ? atoi(e) : 0; }();
   ConvGemmArgs a = args;
   if (env_kmul > 0) a.krot = env_kmul;
+  static const int env_nrot = [] { const char* e = getenv("KDL_WS_NROT"); return e ? atoi(e) : 0; }();
+  if (env_nrot > 0) a.wimg = -1;
   int bm, bn, th;
   // ids 9 / 10 (ablation bit 2, no pointwise MFMA) faulted the GPU once in round 2 (cause not
   // found); refused until understood -- they are timing ablations, never candidates
