@@ -134,16 +134,6 @@ ChScaleArgs chs_args(const py::dict& d) {
   a.B = I(d, "B"); a.HW = I(d, "HW"); a.C = I(d, "C");
   return a;
 }
-MbedArgs mb_args(const py::dict& d) {
-  MbedArgs a{};
-  a.x = P<const uint16_t>(d, "x"); a.we = P<const uint16_t>(d, "we"); a.be = P<const float>(d, "be");
-  a.wd = P<const float>(d, "wd"); a.bd = P<const float>(d, "bd"); a.y = P<uint16_t>(d, "y");
-  a.pool = P<float>(d, "pool"); a.w1 = P<const float>(d, "w1"); a.blob = P<const void>(d, "blob");
-  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.ldx = I(d, "ldx"); a.cin = I(d, "cin");
-  a.C = I(d, "C"); a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.K = I(d, "K"); a.S = I(d, "S");
-  a.pad = I(d, "pad"); a.Cs = I(d, "Cs"); a.abl = I(d, "abl");
-  return a;
-}
 WScaleArgs ws_args(const py::dict& d) {
   WScaleArgs a{};
   a.w = P<const uint16_t>(d, "w"); a.scale = P<const float>(d, "scale"); a.y = P<uint16_t>(d, "y");
@@ -228,7 +218,6 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(hipMemcpyAsync((void*)dst, (const void*)src, n, (hipMemcpyKind)kind, S(s)), "memcpy_async");
   });
-  m.def("sepconv_pipe_fits", &sepconv_pipe_fits);
   m.def("dw3x3", [](py::dict d, uintptr_t s) {
     const auto a = dw_args(d);
     py::gil_scoped_release nogil;
@@ -300,18 +289,6 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(channel_scale(a, S(s)), "channel_scale");
   });
-  m.def("mbconv_ed", [](py::dict d, uintptr_t s) {
-    const auto a = mb_args(d);
-    py::gil_scoped_release nogil;
-    chk(mbconv_ed(a, S(s)), "mbconv_ed");
-  });
-  m.def("mbconv_ed_tiles", [](py::dict d) {
-    const auto a = mb_args(d);
-    int rb, tw, nt;
-    mbconv_ed_tiles(a, &rb, &tw, &nt);
-    return py::make_tuple(rb, tw, nt);
-  });
-  m.def("mbconv_blob_bytes", [](int cin, int K, int Cs) { return mbconv_blob_bytes(cin, K, Cs); });
   m.def("weight_scale", [](py::dict d, uintptr_t s) {
     const auto a = ws_args(d);
     py::gil_scoped_release nogil;
@@ -326,10 +303,6 @@ PYBIND11_MODULE(_C, m) {
     int bm = 0, bn = 0, th = 0;
     if (gemm_f8_config(cfg, &bm, &bn, &th) != 0) throw std::out_of_range("bad gemm_f8 config");
     return py::make_tuple(bm, bn, th);
-  });
-  m.def("mfma_f8_probe", [](uintptr_t a, uintptr_t b, uintptr_t d, uintptr_t s) {
-    chk(mfma_f8_probe(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
-                      reinterpret_cast<float*>(d), S(s)), "mfma_f8_probe");
   });
   m.def("fc_mfma", [](py::dict d, uintptr_t s) {
     const auto a = fcm_args(d);
@@ -385,9 +358,6 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_se", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_SE; op.name = name; op.se = se_args(d); p.add(op);
-      })
-      .def("add_mbconv_ed", [](Program& p, const std::string& name, py::dict d) {
-        Op op; op.kind = OP_MBED; op.name = name; op.mb = mb_args(d); p.add(op);
       })
       .def("add_wscale", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_WSCALE; op.name = name; op.ws = ws_args(d); p.add(op);

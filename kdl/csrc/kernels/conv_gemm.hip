@@ -302,8 +302,8 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   }
   if (cfg >= C3_CFG_BASE) return mode == MODE_CONV ? conv3x3_2d(cfg - C3_CFG_BASE, a, s) : hipErrorInvalidValue;
   if (cfg >= S2D_CFG_BASE) return mode == MODE_DW ? sepconv_2d(cfg - S2D_CFG_BASE, a, s) : hipErrorInvalidValue;
-  if (cfg >= SEPP_CFG_BASE) return mode == MODE_DW ? sepconv_pipe(cfg - SEPP_CFG_BASE, a, s) : hipErrorInvalidValue;
-  if (cfg >= SEP_CFG_BASE) return mode == MODE_DW ? sepconv_fused(cfg - SEP_CFG_BASE, a, s) : hipErrorInvalidValue;
+  if (cfg >= SEPW_CFG_BASE) return mode == MODE_DW ? sepconv_ws(cfg - SEPW_CFG_BASE, a, s) : hipErrorInvalidValue;
+  if (cfg >= SEP_CFG_BASE) return hipErrorInvalidValue;
   if (cfg >= PIPE_CFG_BASE) return gemm_pipe(mode, cfg - PIPE_CFG_BASE, a, s);
   switch (mode) {
     case MODE_PW: return launch_mode<MODE_PW>(cfg, a, s);
@@ -316,8 +316,8 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
 int conv_gemm_config(int cfg, int* bm, int* bn, int* threads) {
   if (cfg >= C3_CFG_BASE) return conv3x3_2d_config(cfg - C3_CFG_BASE, bm, bn, threads);
   if (cfg >= S2D_CFG_BASE) return sepconv_2d_config(cfg - S2D_CFG_BASE, bm, bn, threads);
-  if (cfg >= SEPP_CFG_BASE) return sepconv_pipe_config(cfg - SEPP_CFG_BASE, bm, bn, threads);
-  if (cfg >= SEP_CFG_BASE) return sepconv_fused_config(cfg - SEP_CFG_BASE, bm, bn, threads);
+  if (cfg >= SEPW_CFG_BASE) return sepconv_ws_config(cfg - SEPW_CFG_BASE, bm, bn, threads);
+  if (cfg >= SEP_CFG_BASE) return -1;
   if (cfg >= PIPE_CFG_BASE) return gemm_pipe_config(cfg - PIPE_CFG_BASE, bm, bn, threads);
   switch (cfg) {
 #define KDL_INFO(id, fm, fn, wgm, wgn) \

@@ -12,7 +12,7 @@ struct ConvGemmArgs {
   const uint16_t* wp;    // packed weights [NF][K/32][64][8] bf16 (BN scale folded)
   const float* bias;     // [NF*16] fp32 (BN shift)
   const float* dww;      // MODE_DW: depthwise weights [9][K] fp32
-  const uint16_t* dwk;   // MODE_DW, sepconv_pipe: the same weights as bf16 entries [K/32][2][16][2][8]
+  const uint16_t* dwk;   // MODE_DW, sepconv_ws / sepconv_2d: the same weights as bf16 entries [K/32][2][16][2][8]
                          //   (k-step, channel group, channel, tap parity, taps parity+2j)
   const uint16_t* res;   // optional residual [M][ldr] bf16
   uint16_t* y;           // output [M][ldy] bf16 (or a zero-bordered [B][OH+2][OW+2][ldy] if opad)
@@ -52,18 +52,15 @@ struct ConvGemmArgs {
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);
 // cfg >= PIPE_CFG_BASE: LDS-DMA pipelined kernel (MODE_PW / MODE_CONV only).
 constexpr int PIPE_CFG_BASE = 16;
-// cfg >= SEP_CFG_BASE: fused separable conv (MODE_DW only, sepconv_fused.hip).
+// cfg >= SEP_CFG_BASE: fused separable convs (MODE_DW only). Ids 64..119 are retired (the
+// round-1/2 sepconv_fused / sepconv_pipe kernels, measured slower than sepconv_ws / sepconv_2d
+// on every Xception shape and removed in round 3).
 constexpr int SEP_CFG_BASE = 64;
-hipError_t sepconv_fused(int cfg, const ConvGemmArgs& a, hipStream_t s);
-// cfg >= SEPP_CFG_BASE: LDS-DMA pipelined fused separable conv (MODE_DW only, sepconv_pipe.hip).
-constexpr int SEPP_CFG_BASE = 96;
-hipError_t sepconv_pipe(int cfg, const ConvGemmArgs& a, hipStream_t s);
-int sepconv_pipe_config(int cfg, int* bm, int* bn, int* threads);
-int sepconv_pipe_fits(int cfg, int W);
-hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);     // ids SEPP_CFG_BASE + 24 ..
+// cfg >= SEPW_CFG_BASE: warp-specialized fused separable conv (sepconv_ws.hip).
+constexpr int SEPW_CFG_BASE = 120;
+hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_ws_fits(int cfg, int W);
-int sepconv_fused_config(int cfg, int* bm, int* bn, int* threads);
 // cfg >= C3_CFG_BASE: 3x3 'valid' conv over 2-D tiles with an LDS halo patch (MODE_CONV, cin 32 only,
 // conv3x3_2d.hip: Xception block1_conv2).
 constexpr int C3_CFG_BASE = 208;
@@ -224,25 +221,6 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s);
 void dwk_tiles(const DwkArgs& a, int* cg, int* rb, int* tw, int* ntiles);
 int dwk_seg(const DwkArgs& a);
 
-// Fused MBConv front half (mbconv.hip): expand 1x1 + BN + SiLU -> KxK/S depthwise + BN + SiLU
-// -> SE pool / fc1 partials, the expanded tensor staying in LDS.
-struct MbedArgs {
-  const uint16_t* x;      // [B][H][W][ldx] block input
-  const uint16_t* we;     // expand weights, packed fragments [C/16 (+pad)][cin/32][64][8]
-  const float* be;        // [C] expand bias
-  const float* wd;        // [K*K][C] depthwise weights fp32 (BN folded)
-  const float* bd;        // [C] depthwise bias
-  uint16_t* y;            // [B][OH][OW][C] depthwise output
-  float* pool;            // [B][ntiles][Cs] fc1 partials
-  const float* w1;        // [Cs][C]
-  const void* blob;       // per-channel-block parameter blobs [C/32][mbconv_blob_bytes] (mbconv.hip)
-  int B, H, W, ldx, cin, C, OH, OW, K, S, pad, Cs;
-  int abl;                // timing ablations (tools only): 1 no depthwise, 2 no expand MFMA, 4 no reductions
-};
-hipError_t mbconv_ed(const MbedArgs& a, hipStream_t s);
-void mbconv_ed_tiles(const MbedArgs& a, int* rb, int* tw, int* ntiles);
-int mbconv_blob_bytes(int cin, int K, int Cs);
-
 // Squeeze-excite tail: scale[b][c] = sigmoid(W2 SiLU(sum_parts pool / HW + b1) + b2).
 struct SeArgs {
   const float* pool;      // [B][ntiles][Cs] fc1 partials from dwk
@@ -286,9 +264,6 @@ struct GemmF8Args {
 };
 hipError_t gemm_f8(int cfg, const GemmF8Args& a, hipStream_t s);
 int gemm_f8_config(int cfg, int* bm, int* bn, int* threads);
-
-// Debug: one v_mfma_scale_f32_16x16x128_f8f6f4 on lane-ordered operands (64 x 32 B each).
-hipError_t mfma_f8_probe(const void* a, const void* b, float* d, hipStream_t s);
 
 // Classifier head: GAP over HW -> dense(F->H1)+ReLU -> dense(H1->NC), fp32 logits.
 struct HeadArgs {

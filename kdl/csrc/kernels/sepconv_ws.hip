@@ -43,7 +43,7 @@ __device__ __forceinline__ void ws_wait_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int FM, int FN, int STAGES, int XB, bool STAMP, int ABL, bool RELU>
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU>
 __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   constexpr int NT = 512;
   constexpr int BM = 16 * FM, BN = 64 * FN;
@@ -80,11 +80,11 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   // band: raster pixels P0 .. P0+NS-1 = every 3x3 neighbour of the tile's pixels, as 4
   // planes (one per 8-channel chunk) of NSP 16-byte slots; slot NSP-1 stays zero
   const long P0 = (long)m0 - W - 1;
-  // ABL bit 32: every M tile walks K from its own starting chunk (the two N tiles of an M
-  // tile share it, so their band reads stay L2-shared): without it all workgroups fetch the
+  // KROT: every M tile walks K from its own starting chunk (the two N tiles of an M tile
+  // share it, so their band reads stay L2-shared): without it all workgroups fetch the
   // same weight fragments at the same time
   int krot = 0;
-  if constexpr ((ABL & 32) != 0) {
+  if constexpr (KROT) {
     // a.krot: multiplier (probes); a.wimg (unused by ws) < 0: the N tiles of an M tile also
     // start half a K loop apart (KDL_WS_NROT probe)
     krot = (mi * (a.krot > 0 ? a.krot : 7) + (a.wimg < 0 ? ni * (KT / 2) : 0)) % KT;
@@ -125,11 +125,6 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
       long p = P0 + slot;
       p = p < 0 ? 0 : (p >= NPIX ? NPIX - 1 : p);
       xsrc[i] = slot < NS ? (const uint8_t*)(a.x + p * a.ldx + q * 8) : sepw_zeros;
-      if constexpr (ABL & 16) {                  // timing ablation: 16 pixels x 64 B per instruction
-        long pr = P0 + min(wn + 4 * i, XB - 1) * 16 + (lane >> 2);
-        pr = pr < 0 ? 0 : (pr >= NPIX ? NPIX - 1 : pr);
-        xsrc[i] = (const uint8_t*)(a.x + pr * a.ldx + (lane & 3) * 8);
-      }
     }
     // stages past the end (the branch-free loop keeps issuing) re-load the last one (a scalar
     // clamp; a per-lane select to a zero block cost more VALU than the drain it saves)
@@ -139,7 +134,13 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
       for (int i = 0; i < LCB; ++i) glds16(xsrc[i] + t * 64, smem + slot * STAGE + min(wn + 4 * i, XB - 1) * 1024);
     };
     // B loads as inline asm: the compiler's waitcnt pass does not track them (it inserted a
-    // conservative vmcnt(0) before their first use each iteration); the counted wait above covers them
+    // conservative vmcnt(0) before their first use each iteration); the counted wait above covers them.
+    // CONTRACT: every such load must be covered by ws_wait_barrier<WC> before ANY instruction
+    // touches its destination registers, and every dword of each destination must stay live
+    // until its MFMA (the compiler believes the asm wrote the register at issue: a dword it sees
+    // as dead is re-allocated while the load is still in flight -- that was the round-2 GPU
+    // fault of the removed "no pointwise MFMA" timing ablation, which read one dword of each
+    // fragment). tools/vmcnt_check.py proves it on the built code (tests/test_vmcnt_hazards.py).
     auto gload = [&](s16x8& dst, const uint8_t* p) {
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
     };
@@ -154,18 +155,14 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
       s16x8 af[FM];
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(As + i * 1024);
-      if constexpr (!(ABL & 4)) issue_band(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      issue_band(t + STAGES - 1, (t + STAGES - 1) % STAGES);
       // B(t) is consumed fragment by fragment; each register set is refilled with B(t+2)
       // right behind its last MFMA
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        if constexpr (ABL & 2) {                  // timing ablation: no pointwise MFMA
-          acc[0][j][0] += __uint_as_float((uint32_t)af[j % FM][0] ^ (uint32_t)b[j][1]);
-        } else {
 #pragma unroll
-          for (int i = 0; i < FM; ++i) acc[i][j] = mfma16(b[j], af[i], acc[i][j]);
-        }
-        if constexpr (!(ABL & 64)) gload(b[j], bsrc + j * bstride + (long)kc(t + 2) * 1024);
+        for (int i = 0; i < FM; ++i) acc[i][j] = mfma16(b[j], af[i], acc[i][j]);
+        gload(b[j], bsrc + j * bstride + (long)kc(t + 2) * 1024);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, FM, 0);      // A fragment reads
 #pragma unroll
@@ -270,12 +267,7 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
 #pragma unroll
             for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
           }
-          if constexpr (ABL & 1) {               // timing ablation: no depthwise MFMA
-            dacc[i][0] += __uint_as_float(v[0] ^ (uint32_t)wf[j][0]);
-            dacc[i][1] += __uint_as_float(v[1] ^ v[2] ^ v[3]);
-          } else {
-            dacc[i] = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc[i]);
-          }
+          dacc[i] = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc[i]);
         }
       const bool live = s < KT;
 #pragma unroll
@@ -296,11 +288,9 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
     for (int t = 0; t < KTE; ++t) {
       ws_wait_barrier<STAGES - 4>();             // stage t+2 landed and published
       stamp(st0, t);
-      if constexpr (!(ABL & 8)) {
-        dw_mfma(t + 1, xv, we, (t + 1) & 1);     // inputs read during the previous step
-        dw_load(t + 2, xv, we);                  // consumed next step
-      }
-      if constexpr (!(ABL & 4)) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      dw_mfma(t + 1, xv, we, (t + 1) & 1);       // inputs read during the previous step
+      dw_load(t + 2, xv, we);                    // consumed next step
+      issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
       if constexpr (STAMP) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stamp(st1, t);
@@ -347,7 +337,10 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
 
 // (FM, FN, STAGES, XB = band KiB): tile BM = 16*FM, BN = 64*FN; LDS = STAGES*(XB+1) KiB + 2FM KiB
 // (+ the BM x BN bf16 C tile, which reuses it); the band needs BM + 2W + 3 <= 16*XB.
-// ids 7..14: s_memtime stamping variants with timing ablations (tools/stamps.py; never tuned).
+// Retired ids (round 3): 8-14, 18, 19, 27 were timing ablations (no depthwise / pointwise MFMA,
+// no loop DMA, wrong band placement, no B reloads). Ablations 2-5 and 12 broke the counted-vmcnt
+// contract above (tools/vmcnt_check.py flags exactly those five builds and no other kernel):
+// the cause of the round-2 fault. Their slots stay reserved so tuning-table ids keep meaning.
 #define KDL_SEPW_CONFIGS(X) \
   X(0, 6, 6, 5, 9)          \
   X(1, 6, 6, 6, 9)          \
@@ -357,37 +350,21 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(5, 4, 6, 5, 8)          \
   X(6, 6, 6, 8, 9)          \
   X(7, 6, 6, 6, 9)          \
-  X(8, 6, 6, 6, 9)          \
-  X(9, 6, 6, 6, 9)          \
-  X(10, 6, 6, 6, 9)         \
-  X(11, 6, 6, 6, 9)         \
-  X(12, 6, 6, 6, 9)         \
-  X(13, 6, 6, 6, 9)         \
-  X(14, 6, 6, 6, 9)          \
-  X(15, 12, 3, 5, 15)        \
-  X(16, 8, 3, 5, 11)         \
-  X(17, 12, 3, 6, 15)        \
-  X(18, 6, 6, 5, 9)          \
-  X(19, 4, 6, 5, 8)          \
-  X(20, 4, 3, 5, 8)          \
-  X(21, 4, 3, 6, 8)          \
-  X(22, 2, 6, 5, 8)          \
-  X(23, 6, 6, 5, 9)          \
-  X(24, 6, 6, 5, 11)         \
-  X(25, 6, 6, 5, 16)         \
-  X(26, 4, 6, 5, 8)          \
-  X(27, 6, 6, 6, 9)
+  X(15, 12, 3, 5, 15)       \
+  X(16, 8, 3, 5, 11)        \
+  X(17, 12, 3, 6, 15)       \
+  X(20, 4, 3, 5, 8)         \
+  X(21, 4, 3, 6, 8)         \
+  X(22, 2, 6, 5, 8)         \
+  X(23, 6, 6, 5, 9)         \
+  X(24, 6, 6, 5, 11)        \
+  X(25, 6, 6, 5, 16)        \
+  X(26, 4, 6, 5, 8)
 
-// timing-ablation bits of the stamping ids: 1 no depthwise MFMA, 2 no pointwise MFMA,
-// 4 no band / weight LDS-DMA in the loop, 8 producers skip the depthwise entirely;
-// ids 18/19 (no stamps): 16 = band DMA'd as 16 pixels x 64 B per instruction (wrong LDS
-// placement for the producers: timing only); ids 23-26 = 0, 2, 3, 5 with bit 32 (per-M-tile
-// rotated K order); id 27 = stamping with bit 64 (consumers never reload their pointwise
-// weight registers: timing only)
-constexpr int sepw_abl(int id) {
-  return id == 8 ? 1 : id == 9 ? 2 : id == 10 ? 3 : id == 11 ? 4 : id == 12 ? 5 : id == 13 ? 8 : id == 14 ? 12
-       : id == 18 || id == 19 ? 16 : id >= 23 && id <= 26 ? 32 : id == 27 ? 64 : 0;
-}
+// id 7: s_memtime stamping variant (tools/stamps.py; never tuned); ids 23-26 = 0, 2, 3, 5
+// walking K from a per-M-tile rotated start
+constexpr bool sepw_stamp(int id) { return id == 7; }
+constexpr bool sepw_krot(int id) { return id >= 23 && id <= 26; }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }
 
@@ -419,9 +396,6 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
   static const int env_nrot = [] { const char* e = getenv("KDL_WS_NROT"); return e ? atoi(e) : 0; }();
   if (env_nrot > 0) a.wimg = -1;
   int bm, bn, th;
-  // ids 9 / 10 (ablation bit 2, no pointwise MFMA) faulted the GPU once in round 2 (cause not
-  // found); refused until understood -- they are timing ablations, never candidates
-  if (cfg == 9 || cfg == 10) return hipErrorInvalidValue;
   if (sepconv_ws_config(cfg, &bm, &bn, &th) != 0 || !sepconv_ws_fits(cfg, a.W) || a.K % 32 != 0 ||
       a.K > 8192 || (a.NF * 16) % bn != 0 || a.OH != a.H || a.OW != a.W || a.M <= 0 || a.dwk == nullptr)
     return hipErrorInvalidValue;
@@ -430,10 +404,10 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
 #define KDL_SWCASE(id, fm, fn, st, xb)                                                                \
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, ((id >= 7 && id <= 14) || id == 27), sepw_abl(id), true>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), true>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     else                                                                                            \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, ((id >= 7 && id <= 14) || id == 27), sepw_abl(id), false>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), false>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)

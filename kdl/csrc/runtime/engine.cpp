@@ -28,7 +28,6 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_SE: return squeeze_excite(op.se, s);
     case OP_CHSCALE: return channel_scale(op.cs, s);
     case OP_WSCALE: return weight_scale(op.ws, s);
-    case OP_MBED: return mbconv_ed(op.mb, s);
     case OP_GEMM_F8: return gemm_f8(op.cfg, op.f8, s);
   }
   return hipErrorInvalidValue;

@@ -17,7 +17,7 @@ namespace kdl {
 
 enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6, OP_GAP = 7, OP_FC = 8, OP_FC_MFMA = 9,
               OP_PATCHIFY = 10, OP_EMBED = 11, OP_LN = 12, OP_ATTN = 13,
-              OP_DWK = 14, OP_SE = 15, OP_CHSCALE = 16, OP_GEMM_F8 = 17, OP_WSCALE = 18, OP_MBED = 19 };
+              OP_DWK = 14, OP_SE = 15, OP_CHSCALE = 16, OP_GEMM_F8 = 17, OP_WSCALE = 18 };
 
 struct Op {
   OpKind kind;
@@ -40,7 +40,6 @@ struct Op {
   SeArgs se{};
   ChScaleArgs cs{};
   WScaleArgs ws{};
-  MbedArgs mb{};
   GemmF8Args f8{};
   void* mem_ptr = nullptr;
   size_t mem_bytes = 0;

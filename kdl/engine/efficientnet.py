@@ -5,9 +5,6 @@ Lowering (captured into one hipGraph per batch bucket):
 
     stem_conv       3x3/2 pad 1, 3 -> 64 + BN + SiLU, mean/std applied on load
     per MBConv (55):
-      mbconv_ed     expand 1x1 + BN + SiLU -> KxK/S depthwise + BN + SiLU -> SE pool/fc1
-                    partials in ONE kernel, the expanded tensor kept in LDS (mbconv.hip;
-                    expand-ratio-6 blocks with cin <= 160: stages 2-4; KDL_MBED=1), else
       conv_gemm PW  expand 1x1 + BN + SiLU                  (expand ratio 6 blocks)
       dwk           KxK/S depthwise + BN + SiLU; SE average pool + squeeze FC fused
                     (per-tile partials of fc1, which is linear in the pooled mean)
@@ -18,6 +15,11 @@ Lowering (captured into one hipGraph per batch bucket):
       conv_gemm PW  project 1x1 + BN (+ identity residual), per-image weights
     conv_gemm PW    head 1x1 640 -> 2560 + BN + SiLU
     gap + fc_mfma   global pool (bf16) -> classifier 2560 -> 1000
+
+(A fused expand + depthwise kernel that kept the expanded tensor in LDS was measured
+2x slower than this unfused pair -- per 32-channel block the workgroup waited a full
+memory round trip for the next block's parameters, profiles/entry_flow_r2.txt -- and
+was removed in round 3.)
 
 Activations are NHWC bf16 with channels padded to multiples of 32 (zeros); the
 largest tensor (stage-2 expand at 300x300x192) is 34.6 MB per image, so at batch
@@ -44,28 +46,6 @@ def _fold(p, conv, bn):
     return w, s, t
 
 
-def mbconv_blobs(lay: ConvGemmLayer, dw: tuple, w1: torch.Tensor, K: int, nbytes: int) -> torch.Tensor:
-    """Per-32-channel-block parameter blobs of the fused MBConv kernel (layout: mbconv.hip):
-    expand B fragments (2cb + j, t) | depthwise weights [K*K][32] | biases expand[32],
-    depthwise[32] | fc1 slice [Cs][32], fp32 except the bf16 fragments, each blob padded to
-    ``nbytes``. One contiguous read per block instead of four scattered ones."""
-    wd, bd = dw
-    KT = lay.K // 32
-    C = wd.shape[1]
-    frags = lay.wp.view(-1, KT, 512)                     # [nf][KT][64 lanes x 8] bf16
-    out = torch.zeros(C // 32, nbytes, dtype=torch.uint8, device=wd.device)
-    for cb in range(C // 32):
-        sl = slice(cb * 32, cb * 32 + 32)
-        parts = [frags[2 * cb:2 * cb + 2].reshape(-1).view(torch.uint8),
-                 wd[:, sl].contiguous().view(torch.uint8).reshape(-1),
-                 lay.bias[sl].contiguous().view(torch.uint8), bd[sl].contiguous().view(torch.uint8),
-                 w1[:, sl].contiguous().view(torch.uint8).reshape(-1)]
-        blob = torch.cat(parts)
-        assert blob.numel() <= nbytes, (blob.numel(), nbytes)
-        out[cb, :blob.numel()] = blob
-    return out.contiguous()
-
-
 class EfficientNetEngine(EngineBase):
     model_name = "efficientnet_b7"
 
@@ -74,10 +54,6 @@ class EfficientNetEngine(EngineBase):
         super().__init__(device, max_batch, buckets)
         self.size = size
         self.sefold = os.environ.get("KDL_SEFOLD", "1") != "0"
-        # fused expand + depthwise (mbconv.hip): off by default until it beats the unfused pair
-        # (first cut: 926 vs 1800 img/s -- per 32-channel block the workgroup waited a full
-        # memory round trip for the next block's parameters; profiles/entry_flow_r2.txt)
-        self.mbed = os.environ.get("KDL_MBED", "0") == "1"
         self.wimg_max = 0                          # largest packed project weight set (elements)
         self.classes = params["classifier.1.bias"].numel()
         self.bufsz: dict[str, int] = {}            # buffer -> elements per image (max over uses)
@@ -106,7 +82,7 @@ class EfficientNetEngine(EngineBase):
         self.steps.append(Step("stem", "stem", src="input", dst="X0", geom=(self.size, self.size, H, H)))
         self._need("X0", H * H * E.STEM)
         cur, ldc, ping = "X0", E.STEM, 0
-        self.dw, self.se, self.expand, self.blobs = {}, {}, {}, {}
+        self.dw, self.se = {}, {}
         C = _lib.lib()
         for blk in E.blocks():
             n = blk.names()
@@ -121,26 +97,13 @@ class EfficientNetEngine(EngineBase):
                                    p[f"{se}.fc1.bias"].float().to(dev),
                                    p[f"{se}.fc2.weight"].reshape(ce, blk.csq).t().float().contiguous().to(dev),
                                    p[f"{se}.fc2.bias"].float().to(dev))
-            geo = dict(B=1, H=H, W=H, ldx=ldc, C=ce, OH=oh, OW=oh, K=blk.k, S=blk.stride,
-                       pad=(blk.k - 1) // 2, Cs=blk.csq)
-            fused = False
             if "expand" in n:
                 lay = self._pw(n["expand"], p, f"{n['expand']}.0.weight", f"{n['expand']}.1", blk.cin, ce, 4)
-                fused = self.mbed and C.mbconv_ed_tiles(dict(geo, cin=lay.cin_pad))[2] > 0
-                if fused:
-                    self.expand[blk.prefix] = lay
-                    self.blobs[blk.prefix] = mbconv_blobs(lay, self.dw[blk.prefix], self.se[blk.prefix][0], blk.k,
-                                                          C.mbconv_blob_bytes(lay.cin_pad, blk.k, blk.csq))
-                    self.steps.append(Step("mbed", f"{blk.prefix}.mbed", src=cur, dst="D", geom=(H, H, oh, oh),
-                                           extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix,
-                                                      ldx=ldc, cin=lay.cin_pad)))
-                else:
-                    self.steps.append(Step("conv", lay.name, lay, cur, "E", geom=(H, H, H, H), extra=dict(ldx=ldc)))
-                    self._need("E", H * H * ce)
-                    src = "E"
-            if not fused:
-                self.steps.append(Step("dwk", f"{blk.prefix}.dw", src=src, dst="D", geom=(H, H, oh, oh),
-                                       extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
+                self.steps.append(Step("conv", lay.name, lay, cur, "E", geom=(H, H, H, H), extra=dict(ldx=ldc)))
+                self._need("E", H * H * ce)
+                src = "E"
+            self.steps.append(Step("dwk", f"{blk.prefix}.dw", src=src, dst="D", geom=(H, H, oh, oh),
+                                   extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
             self._need("D", oh * oh * ce)
             self.steps.append(Step("se", f"{blk.prefix}.se", src="pool", dst="scale", geom=(H, H, oh, oh),
                                    extra=dict(C=ce, Cs=blk.csq, K=blk.k, S=blk.stride, blk=blk.prefix)))
@@ -178,14 +141,11 @@ class EfficientNetEngine(EngineBase):
         self.ntiles = {}
         mx = 1
         for st in self.steps:
-            if st.kind in ("dwk", "mbed"):
+            if st.kind == "dwk":
                 H_, W_, oh_, ow_ = st.geom
                 g = dict(B=1, H=H_, W=W_, C=st.extra["C"], OH=oh_, OW=ow_, K=st.extra["K"], S=st.extra["S"],
                          pad=(st.extra["K"] - 1) // 2, Cs=st.extra["Cs"])
-                if st.kind == "dwk":
-                    nt = C.dwk_tiles(g)[3]
-                else:
-                    nt = C.mbconv_ed_tiles(dict(g, ldx=st.extra["ldx"], cin=st.extra["cin"]))[2]
+                nt = C.dwk_tiles(g)[3]
                 self.ntiles[st.extra["blk"]] = nt
                 mx = max(mx, nt * st.extra["Cs"])
         self.pool_per_image = mx
@@ -240,18 +200,6 @@ class EfficientNetEngine(EngineBase):
                                          y=self._ptr("D"), pool=self._ptr("pool"), w1=_lib.ptr(w1),
                                          Cs=step.extra["Cs"], B=b, H=H, W=W, C=step.extra["C"], OH=OH, OW=OW,
                                          K=K, S=step.extra["S"], pad=(K - 1) // 2, act=2))
-        elif step.kind == "mbed":
-            w, bias = self.dw[step.extra["blk"]]
-            w1 = self.se[step.extra["blk"]][0]
-            lay = self.expand[step.extra["blk"]]
-            K = step.extra["K"]
-            prog.add_mbconv_ed(step.name, dict(x=self._ptr(step.src), blob=_lib.ptr(self.blobs[step.extra["blk"]]),
-                                               we=_lib.ptr(lay.wp), be=_lib.ptr(lay.bias),
-                                               wd=_lib.ptr(w), bd=_lib.ptr(bias), y=self._ptr("D"),
-                                               pool=self._ptr("pool"), w1=_lib.ptr(w1), B=b, H=H, W=W,
-                                               ldx=step.extra["ldx"], cin=step.extra["cin"], C=step.extra["C"],
-                                               OH=OH, OW=OW, K=K, S=step.extra["S"], pad=(K - 1) // 2,
-                                               Cs=step.extra["Cs"]))
         elif step.kind == "se":
             _, b1, w2t, b2 = self.se[step.extra["blk"]]
             prog.add_se(step.name, dict(pool=self._ptr("pool"), b1=_lib.ptr(b1),

@@ -20,7 +20,9 @@ MODE_PW, MODE_CONV, MODE_DW = 0, 1, 2
 # (FM, FN, WGM, WGN): block tile = (16*FM*WGM) x (16*FN*WGN).
 # ids < PIPE_BASE: KDL_CONFIGS in conv_gemm.hip (register-B kernel, supports the
 # fused depthwise producer); ids >= PIPE_BASE: KDL_PIPE_CONFIGS in gemm_pipe.hip
-# (LDS-DMA ring, pointwise / 3x3 only).
+# (LDS-DMA ring, pointwise / 3x3 only); ids >= SEP_BASE: fused separable convs
+# (MODE_DW). Ids 64-119 belonged to the round-1/2 sepconv_fused / sepconv_pipe kernels,
+# retired in round 3 (slower than sepconv_ws / sepconv_2d on every Xception shape).
 PIPE_BASE = 16
 CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4: (4, 6, 1, 8),
            5: (2, 12, 1, 4), 6: (4, 4, 1, 4), 7: (2, 6, 1, 8), 8: (8, 2, 1, 4), 9: (4, 2, 1, 4),
@@ -36,26 +38,14 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            48: (6, 3, 2, 4), 49: (6, 3, 2, 4), 50: (6, 3, 2, 4), 51: (6, 3, 2, 4),
            52: (6, 3, 2, 4), 53: (6, 3, 2, 4), 54: (6, 3, 2, 4), 55: (6, 3, 2, 4), 56: (6, 3, 2, 4),
            57: (6, 3, 2, 4), 58: (6, 3, 2, 4), 59: (6, 3, 2, 4), 60: (6, 3, 2, 4),
-           # ids >= SEP_BASE: fused separable conv (sepconv_fused.hip): (FM, NFW, 1, NW)
-           64: (4, 6, 1, 8), 65: (4, 1, 1, 8), 66: (4, 2, 1, 8), 67: (2, 6, 1, 8), 68: (4, 4, 1, 8),
-           69: (4, 3, 1, 8), 70: (8, 1, 1, 8), 71: (8, 2, 1, 8), 72: (2, 3, 1, 8), 73: (4, 2, 1, 4),
-           74: (4, 1, 1, 4),
-           # ids >= SEPP_BASE: LDS-DMA pipelined fused separable conv (sepconv_pipe.hip)
-           96: (3, 6, 2, 4), 97: (3, 6, 2, 4), 98: (3, 3, 2, 4), 99: (2, 6, 2, 4), 100: (3, 6, 2, 4),
-           101: (3, 3, 2, 4), 102: (2, 6, 2, 4), 103: (2, 3, 2, 4), 104: (3, 3, 2, 4),
-           # timing ablations of 97 (tools/kbench.py --cfgs; never candidates)
-           112: (3, 6, 2, 4), 113: (3, 6, 2, 4), 114: (3, 6, 2, 4), 115: (3, 6, 2, 4), 116: (3, 6, 2, 4),
-           117: (3, 6, 2, 4),
-           # warp-specialized fused separable conv (sepconv_ws.hip): (FM, FN, 1, 4)
+           # warp-specialized fused separable conv (sepconv_ws.hip, KDL_SEPW_CONFIGS): (FM, FN, 1, 4);
+           # 127 = s_memtime stamping build of 121 (tools/stamps.py, never a candidate)
            120: (6, 6, 1, 4), 121: (6, 6, 1, 4), 122: (6, 6, 1, 4), 123: (6, 6, 1, 4), 124: (6, 3, 1, 4),
            125: (4, 6, 1, 4), 126: (6, 6, 1, 4), 127: (6, 6, 1, 4),
-           128: (6, 6, 1, 4), 129: (6, 6, 1, 4), 130: (6, 6, 1, 4),
-           131: (6, 6, 1, 4), 132: (6, 6, 1, 4), 133: (6, 6, 1, 4), 134: (6, 6, 1, 4),
-           135: (12, 3, 1, 4), 136: (8, 3, 1, 4), 137: (12, 3, 1, 4), 138: (6, 6, 1, 4), 139: (4, 6, 1, 4),
+           135: (12, 3, 1, 4), 136: (8, 3, 1, 4), 137: (12, 3, 1, 4),
            140: (4, 3, 1, 4), 141: (4, 3, 1, 4), 142: (2, 6, 1, 4),
-           # 143-146 = 120, 122, 123, 125 walking K from a per-M-tile rotated start (ABL bit 32)
+           # 143-146 = 120, 122, 123, 125 walking K from a per-M-tile rotated start
            143: (6, 6, 1, 4), 144: (6, 6, 1, 4), 145: (6, 6, 1, 4), 146: (4, 6, 1, 4),
-           147: (6, 6, 1, 4),   # stamping + no B reloads (timing only)
            # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
            160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
            165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
@@ -75,20 +65,16 @@ S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188:
 # DMA-wave variant (sepconv_2dw_kernel): no C tile / bias in LDS
 S2DW = {200: (4, 4, 16), 201: (4, 8, 16), 202: (4, 6, 16), 203: (4, 4, 16), 204: (6, 8, 16)}
 SEP_BASE = 64
-SEPP_BASE = 96
 SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
 S2D_BASE = 160    # 2-D spatial tiles (sepconv_2d.hip): the early flow's 147x147 / 74x74 maps
 C3_BASE = 208     # 2-D tiled 3x3 conv, cin 32 (conv3x3_2d.hip): block1_conv2
 S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 48, 19 -> 32)
-# x-band KiB per stage of each KDL_SEPP_CONFIGS entry (mirror of sepconv_pipe_fits)
-SEPP_XB = {96: 12, 97: 12, 98: 12, 99: 12, 100: 16, 101: 16, 102: 20, 103: 20, 104: 12,
-           **{i: 12 for i in range(112, 118)},
-           120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9, 128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 134: 9,
-           135: 15, 136: 11, 137: 15, 138: 9, 139: 8, 140: 8, 141: 8, 142: 8,
-           143: 9, 144: 11, 145: 16, 146: 8, 147: 9}
-ABLATION_IDS = frozenset(list(range(43, 61)) + list(range(112, 118)) + list(range(127, 135)) + [138, 139, 147])   # 127+: s_memtime stamping
-# staged 16-byte chunks per thread of each fused separable config (KDL_SEP_CONFIGS)
-SEP_SPT = {64: 2, 65: 6, 66: 3, 67: 2, 68: 2, 69: 2, 70: 6, 71: 3, 72: 2, 73: 6, 74: 12}
+# x-band KiB per stage of each KDL_SEPW_CONFIGS entry (mirror of sepconv_ws_fits)
+SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
+           135: 15, 136: 11, 137: 15, 140: 8, 141: 8, 142: 8,
+           143: 9, 144: 11, 145: 16, 146: 8}
+# never autotune candidates: gemm_pipe timing ablations (KDL_PIPE_ABL), the ws stamping build
+ABLATION_IDS = frozenset(list(range(43, 61)) + [127])
 
 
 def s2dp_smem(cfg: int, K: int) -> int:
@@ -103,7 +89,7 @@ def s2dp_smem(cfg: int, K: int) -> int:
 
 
 def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | None = None) -> bool:
-    """Mirror of the host-side launch checks in sepconv_fused.hip / sepconv_pipe.hip / sepconv_2d.hip."""
+    """Mirror of the host-side launch checks in sepconv_ws.hip / sepconv_2d.hip / conv3x3_2d.hip."""
     if cfg >= C3_BASE:    # one N tile of all outputs, 32 input channels (K = 288)
         return (K is None or K == 288) and (n is None or round_up(n, cfg_tile(cfg)[1]) == cfg_tile(cfg)[1])
     if cfg < SEP_BASE or W is None:
@@ -114,17 +100,8 @@ def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | No
     if cfg >= S2D_BASE:
         return W >= S2D_MIN_W
     if cfg >= SEPW_BASE:
-        return cfg_tile(cfg)[0] + 2 * W + 3 <= SEPP_XB[cfg] * 16
-    if cfg >= SEPP_BASE:
-        bm = cfg_tile(cfg)[0]
-        return ((bm + W - 2) // W + 3) * W + 1 <= SEPP_XB[cfg] * 16
-    fm, nfw, _, nw = CONFIGS[cfg]
-    bm, bn = 16 * fm, 16 * nfw * nw
-    maxr = (bm - 1) // W + 4
-    if maxr * W * 4 > SEP_SPT[cfg] * 64 * nw:
-        return False
-    pipe = 2 * maxr * W * 64 + 2 * bm * 64 + 2 * 288 * 4
-    return max(pipe, bm * (bn * 2 + 16)) <= 160 * 1024
+        return cfg_tile(cfg)[0] + 2 * W + 3 <= SEPW_XB[cfg] * 16
+    return False
 
 
 def cfg_tile(cfg: int) -> tuple[int, int]:
@@ -310,9 +287,10 @@ class ConvGemmLayer:
 
 
 def pack_dw_entries(dww: torch.Tensor) -> torch.Tensor:
-    """Depthwise weights [9][C] -> sepconv_pipe's per-k-step weight entries, bf16
-    [C/32][g 2][n 16][parity 2][8]: entry (g, n, p) holds w[p + 2j][32t + 16g + n] for
-    j = 0..4 (0 past tap 8), one 16-byte LDS read per lane (sepconv_pipe.hip)."""
+    """Depthwise weights [9][C] -> the per-k-step weight entries of the fused separable
+    kernels, bf16 [C/32][g 2][n 16][parity 2][8]: entry (g, n, p) holds w[p + 2j][32t + 16g + n]
+    for j = 0..4 (0 past tap 8), one 16-byte LDS read per lane (sepconv_ws.hip: the depthwise
+    3x3 as a block-diagonal 16x16x32 MFMA B operand)."""
     C = dww.shape[1]
     w = torch.cat([dww.float(), torch.zeros(1, C)], 0)          # taps 0..9
     w = w.view(5, 2, C // 32, 2, 16)                           # [j][parity][t][g][n]

@@ -64,51 +64,6 @@ def test_dwk_silu_and_fused_squeeze_excite(K, S, H, C, tile):
     assert _rel(y, y0.float() * scale[:, None, None, :]) < 1e-2
 
 
-@pytest.mark.parametrize("cin,C,K,S,H", [(64, 192, 3, 2, 61), (64, 288, 3, 1, 40), (96, 288, 5, 2, 45),
-                                          (96, 480, 5, 1, 23), (160, 960, 3, 1, 19)])
-def test_mbconv_fused_expand_depthwise_matches_unfused(cin, C, K, S, H):
-    """mbconv_ed (expand 1x1 + SiLU -> KxK/S depthwise + SiLU -> SE fc1 partials, the expanded
-    tensor in LDS) == expand conv_gemm + dwk on the same weights: the depthwise output and
-    the per-image fc1 sums (the partials' tiling differs, their sum per image may not)."""
-    from kdl.ops.conv import MODE_PW, ConvGemmLayer, Geometry
-    gen = torch.Generator().manual_seed(cin + C + K + H)
-    B, Cs = 2, max(1, C // 24)
-    pad = (K - 1) // 2
-    OH = (H + 2 * pad - K) // S + 1
-    x = (torch.randn(B, H, H, cin, generator=gen) * 0.5).to(torch.bfloat16).to(DEV).contiguous()
-    we = torch.randn(C, cin, generator=gen, dtype=torch.float64) / cin ** 0.5
-    lay = ConvGemmLayer("exp", MODE_PW, we, torch.randn(C, generator=gen) * 0.1, cin_pad=cin, n=C, relu_out=4,
-                        device=DEV)
-    wk = (torch.randn(K * K, C, generator=gen) / K).to(DEV).contiguous()
-    bd = (torch.randn(C, generator=gen) * 0.1).to(DEV)
-    w1 = (torch.randn(Cs, C, generator=gen) / C ** 0.5).to(DEV).contiguous()
-    C_ = _lib.lib()
-    s = _lib.stream_ptr()
-    geo = dict(B=B, H=H, W=H, C=C, OH=OH, OW=OH, K=K, S=S, pad=pad, Cs=Cs)
-    # unfused reference path
-    e = torch.zeros(B * H * H * lay.ldy, dtype=torch.bfloat16, device=DEV)
-    lay.launch(x.view(-1), e, Geometry(B, H, H, H, H))
-    y0 = torch.zeros(B, OH, OH, C, dtype=torch.bfloat16, device=DEV)
-    nt0 = C_.dwk_tiles(geo)[3]
-    pool0 = torch.zeros(B, nt0, Cs, device=DEV)
-    C_.dwk(dict(geo, x=e.data_ptr(), w=wk.data_ptr(), bias=bd.data_ptr(), y=y0.data_ptr(),
-                pool=pool0.data_ptr(), w1=w1.data_ptr(), act=2), s)
-    # fused
-    from kdl.engine.efficientnet import mbconv_blobs
-    blob = mbconv_blobs(lay, (wk, bd), w1, K, C_.mbconv_blob_bytes(cin, K, Cs))
-    mg = dict(geo, ldx=cin, cin=cin, blob=blob.data_ptr())
-    rb, tw, nt = C_.mbconv_ed_tiles(mg)
-    assert nt > 0, (rb, tw)
-    y1 = torch.full((B, OH, OH, C), float("nan"), dtype=torch.bfloat16, device=DEV)
-    pool1 = torch.zeros(B, nt, Cs, device=DEV)
-    C_.mbconv_ed(dict(mg, x=x.data_ptr(), we=lay.wp.data_ptr(), be=lay.bias.data_ptr(), wd=wk.data_ptr(),
-                      bd=bd.data_ptr(), y=y1.data_ptr(), pool=pool1.data_ptr(), w1=w1.data_ptr()), s)
-    torch.cuda.synchronize()
-    assert not torch.isnan(y1.float()).any()
-    assert _rel(y1, y0) < 2e-2, _rel(y1, y0)
-    assert _rel(pool1.sum(1), pool0.sum(1)) < 2e-2
-
-
 def test_efficientnet_engine_matches_oracle():
     from kdl.engine.efficientnet import EfficientNetEngine
     S = 256

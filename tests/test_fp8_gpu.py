@@ -1,5 +1,5 @@
-"""gfx950 block-scaled fp8 MFMA (OCP e4m3) lane map, determined with exact
-small-integer data, and the fp8 GEMM path built on it."""
+"""The gfx950 block-scaled fp8 (OCP e4m3) GEMM path: gemm_f8.hip against a dequantized
+fp32 reference (which also pins the MFMA operand lane order the kernel stages in)."""
 import pytest
 import torch
 
@@ -7,62 +7,6 @@ from kdl.ops import _lib
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-
-
-def _kmap(name):
-    """k index of byte j (0..31) of lane group g (= lane >> 4) under a candidate map."""
-    if name == "contig32":
-        return lambda g, j: 32 * g + j
-    if name == "split16":
-        return lambda g, j: 16 * g + j if j < 16 else 64 + 16 * g + (j - 16)
-    if name == "interleave8":
-        return lambda g, j: 8 * g + (j % 8) + 32 * (j // 8)
-    raise KeyError(name)
-
-
-def _pack(A, B, km):
-    """A [16][128], B [128][16] small ints -> lane-ordered e4m3 bytes [64][32] each."""
-    a = torch.zeros(64, 32)
-    b = torch.zeros(64, 32)
-    for lane in range(64):
-        g, r = lane >> 4, lane & 15
-        for j in range(32):
-            a[lane, j] = A[r, km(g, j)]
-            b[lane, j] = B[km(g, j), r]
-    enc = lambda t: t.to(torch.float8_e4m3fn).view(torch.uint8)  # noqa: E731
-    return enc(a).contiguous(), enc(b).contiguous()
-
-
-def probe_layout():
-    gen = torch.Generator().manual_seed(0)
-    A = torch.randint(-2, 3, (16, 128), generator=gen).float()
-    B = torch.randint(-2, 3, (128, 16), generator=gen).float()
-    ref = A @ B
-    found = []
-    for name in ("contig32", "split16", "interleave8"):
-        a, b = _pack(A, B, _kmap(name))
-        d = torch.zeros(64, 4, device=DEV)
-        ad, bd = a.to(DEV), b.to(DEV)
-        _lib.lib().mfma_f8_probe(ad.data_ptr(), bd.data_ptr(), d.data_ptr(), _lib.stream_ptr())
-        torch.cuda.synchronize()
-        D = torch.zeros(16, 16)
-        dc = d.cpu()
-        for lane in range(64):
-            for r in range(4):
-                D[4 * (lane >> 4) + r, lane & 15] = dc[lane, r]
-        if torch.equal(D, ref):
-            found.append(name)
-    return found
-
-
-def test_fp8_mfma_lane_map():
-    """Any k bijection shared by A and B gives the same product, so all candidates
-    reproduce A.B; what this pins down is the row/column (lane & 15) and C/D maps and
-    that 'contig32' (lane group g holds k = 32g .. 32g+31) -- the order gemm_f8.hip
-    stages both operands in -- is a valid operand order."""
-    found = probe_layout()
-    print("fp8 16x16x128 consistent lane maps:", found)
-    assert "contig32" in found, found
 
 
 @pytest.mark.parametrize("M,K,N,relu,res", [(300, 768, 2304, 0, False), (197 * 2, 3072, 768, 0, True),

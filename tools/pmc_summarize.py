@@ -1,4 +1,4 @@
-"""Sum rocprofv3 --pmc counter_collection.csv files per kernel (tools/pmc_s5.sh output).
+"""Sum rocprofv3 --pmc counter_collection.csv files per kernel (tools/pmc_cmd.sh output).
 
 python tools/pmc_summarize.py gpurun_out/pmc_s5 > profiles/<name>.txt
 """
