@@ -1,11 +1,12 @@
 # Serving gateway image (gateway.dockerfile:1-17). Torch-free: only the HTTP ->
 # gRPC bridge, Xception preprocessing and the runtime-built TF-Serving protos.
 #   docker build -f deploy/gateway.dockerfile -t model-serving:serving-gateway .
-FROM python:3.10-slim
+FROM python:3.10.12-slim
 
 ENV PYTHONUNBUFFERED=TRUE
 
-RUN pip --no-cache-dir install flask gunicorn grpcio protobuf pillow numpy
+COPY deploy/requirements-gateway.lock /tmp/requirements.lock
+RUN pip --no-cache-dir install --no-deps -r /tmp/requirements.lock
 
 WORKDIR /app
 COPY kdl/__init__.py kdl/labels.py ./kdl/

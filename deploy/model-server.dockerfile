@@ -1,7 +1,9 @@
 # MI355X model server image (replaces `FROM tensorflow/serving:2.3.0`, tf-serving.dockerfile:1-5).
 # Base: ROCm 7 + PyTorch-ROCm. Build from the repo root:
 #   docker build -f deploy/model-server.dockerfile -t model-serving:kdl-model-server .
-FROM rocm/pytorch:latest
+# pinned base (ROCm 7.2 runtime, PyTorch 2.10.0+rocm7.0, Python 3.10) -- the environment every
+# test and benchmark in this repo ran in; never a floating tag
+FROM rocm/pytorch:rocm7.2_ubuntu22.04_py3.10_pytorch_release_2.10.0
 
 ENV PYTHONUNBUFFERED=TRUE \
     HSA_ENABLE_IPC_MODE_LEGACY=0 \
@@ -9,7 +11,8 @@ ENV PYTHONUNBUFFERED=TRUE \
     MODEL_NAME=clothing-model \
     MODEL_BASE_PATH=/models
 
-RUN pip --no-cache-dir install grpcio protobuf safetensors pillow numpy
+COPY deploy/requirements-model-server.lock /tmp/requirements.lock
+RUN pip --no-cache-dir install --no-deps -r /tmp/requirements.lock
 
 WORKDIR /opt/kdl
 COPY kdl ./kdl

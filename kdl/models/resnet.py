@@ -120,8 +120,8 @@ def init_params(seed: int = 0, num_classes: int = NUM_CLASSES, calibrate: bool =
 def preprocess(x_u8_nhwc: torch.Tensor) -> torch.Tensor:
     """uint8 NHWC -> normalised fp32 NCHW (torchvision transforms.Normalize)."""
     x = x_u8_nhwc.float().permute(0, 3, 1, 2) / 255.0
-    mean = torch.tensor(MEAN).view(1, 3, 1, 1)
-    std = torch.tensor(STD).view(1, 3, 1, 1)
+    mean = torch.tensor(MEAN, device=x_u8_nhwc.device).view(1, 3, 1, 1)
+    std = torch.tensor(STD, device=x_u8_nhwc.device).view(1, 3, 1, 1)
     return (x - mean) / std
 
 

@@ -82,7 +82,7 @@ def init_params(seed: int = 0, num_classes: int = NUM_CLASSES) -> dict[str, torc
 
 def preprocess(x_u8_nhwc: torch.Tensor) -> torch.Tensor:
     x = x_u8_nhwc.float().permute(0, 3, 1, 2) / 255.0
-    return (x - torch.tensor(MEAN).view(1, 3, 1, 1)) / torch.tensor(STD).view(1, 3, 1, 1)
+    return (x - torch.tensor(MEAN, device=x.device).view(1, 3, 1, 1)) / torch.tensor(STD, device=x.device).view(1, 3, 1, 1)
 
 
 def embed(p, x_nchw):

@@ -442,10 +442,10 @@ class SignatureRunner:
         self.faults = FaultInjector()
         if devices:
             for d in devices:
-                for _ in range(max(1, cfg.executors_per_gpu)):
+                for _ in range(cfg.executors_for(len(devices))):
                     self.executors.append(GPUExecutor(self, d, cfg.engine_kwargs()))
         else:
-            for i in range(max(1, cfg.executors_per_gpu)):
+            for i in range(cfg.executors_for(1)):
                 self.executors.append(CPUExecutor(self, i))
         for ex in self.executors:
             ex.start()

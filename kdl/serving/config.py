@@ -20,6 +20,8 @@ class BatchingParams:
     max_batch_size: int = 32
     batch_timeout_micros: int = 2000
     max_enqueued_batches: int = 1000
+    # TF-Serving: threads that process batches concurrently. kdl: concurrent batch executors,
+    # spread over the GPUs (ServerConfig.executors_for); --executors_per_gpu overrides it
     num_batch_threads: int = 1
     allowed_batch_sizes: list[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 32])
     # kdl extension (not a TF-Serving knob): an executor whose device is idle takes whatever is
@@ -57,7 +59,7 @@ class ServerConfig:
     rest_api_num_threads: int = 16
     device: str = "auto"          # auto | cpu | gpu
     gpus: int = 0                 # 0 = all visible
-    executors_per_gpu: int = 1
+    executors_per_gpu: int = 0    # 0 = derive from batching.num_batch_threads (executors_for)
     synthetic: bool = False       # random-init weights when the repo has no artifact
     labels: list[str] = field(default_factory=list)
     host: str = "0.0.0.0"
@@ -67,6 +69,15 @@ class ServerConfig:
     stages: str = ""              # stage-pipeline cut ("" = the family's default, "none" = off)
     lanes: int = 1                # split-batch hipGraph lanes for the top bucket
     exec_depth: int = 2           # batches in flight per GPU executor
+
+    def executors_for(self, n_devices: int) -> int:
+        """Executors per device: --executors_per_gpu when given, else TF-Serving's
+        num_batch_threads (batches processed concurrently) spread over the devices."""
+        if self.executors_per_gpu > 0:
+            return self.executors_per_gpu
+        # derived counts stop at 2 per GPU: each executor keeps a compute and a copy stream
+        # busy, and a process gets GPU_MAX_HW_QUEUES = 4 hardware queues per device
+        return min(2, max(1, -(-self.batching.num_batch_threads // max(1, n_devices))))
 
     def engine_kwargs(self) -> dict:
         return {"graph": self.graph, "stages": self.stages, "lanes": self.lanes, "depth": self.exec_depth}
@@ -86,7 +97,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--rest_api_num_threads", type=int, default=16)
     ap.add_argument("--device", choices=["auto", "cpu", "gpu"], default="auto")
     ap.add_argument("--gpus", type=int, default=0)
-    ap.add_argument("--executors_per_gpu", type=int, default=1)
+    ap.add_argument("--executors_per_gpu", type=int, default=0,
+                    help="batch executors per GPU (default: num_batch_threads of the batching "
+                         "parameters file spread over the GPUs, at least 1)")
     ap.add_argument("--max_batch_size", type=int, default=None)
     ap.add_argument("--batch_timeout_micros", type=int, default=None)
     ap.add_argument("--eager_dispatch", default="true",

@@ -116,6 +116,9 @@ def test_conv_gemm_conv3x3():
     (64, 128, 74, False, True, False),
     (128, 128, 67, True, False, True),
     (256, 256, 70, True, True, False),
+    # the headline's 147x147 block2 layers (bench table: sepconv_2dp / sepconv_2dw ids 185 / 204)
+    (64, 128, 147, False, True, False),
+    (128, 128, 147, True, False, False),
 ])
 def test_conv_gemm_separable(cin, n, H, relu_in, relu_out, with_res):
     gen = torch.Generator().manual_seed(3)

@@ -56,3 +56,22 @@ def test_dockerfiles():
     assert "MODEL_NAME=clothing-model" in ms and "/models/clothing-model/1" in ms and "kdl.serving" in ms
     gw = (DEPLOY / "gateway.dockerfile").read_text()
     assert "gunicorn" in gw and "9696" in gw and "kdl.gateway.wsgi:app" in gw
+
+
+def test_images_and_dependencies_are_pinned():
+    """Like the reference's Pipfile.lock (Pipfile:8-17): no floating base tags, every pip
+    dependency pinned to an exact version, and the lock files cover what the code imports."""
+    import re
+    for name, lock in (("model-server.dockerfile", "requirements-model-server.lock"),
+                       ("gateway.dockerfile", "requirements-gateway.lock")):
+        df = (DEPLOY / name).read_text()
+        base = re.search(r"^FROM\s+(\S+)", df, re.M).group(1)
+        assert ":" in base and not base.endswith(":latest"), base
+        assert f"deploy/{lock}" in df and "--no-deps -r" in df
+        pins = [ln.strip() for ln in (DEPLOY / lock).read_text().splitlines()
+                if ln.strip() and not ln.startswith("#")]
+        assert pins and all(re.fullmatch(r"[A-Za-z0-9_.\-]+==[0-9][0-9A-Za-z.+\-]*", p) for p in pins), pins
+        names = {p.split("==")[0].lower() for p in pins}
+        need = {"grpcio", "protobuf", "numpy", "pillow"} | ({"flask", "gunicorn", "werkzeug"} if "gateway" in name
+                                                            else {"safetensors"})
+        assert need <= names, need - names

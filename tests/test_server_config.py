@@ -49,3 +49,17 @@ def test_dtype_selects_engine_variant():
         registry.variant("xception", "fp8")
     with pytest.raises(SystemExit):
         config_from_args(["--dtype", "int4"], env={})
+
+
+def test_num_batch_threads_sets_concurrent_executors(tmp_path):
+    """TF-Serving's num_batch_threads (batches processed concurrently) is honoured: it sets the
+    executor count, spread over the GPUs, unless --executors_per_gpu is given."""
+    from kdl.serving.config import config_from_args
+    f = tmp_path / "batching.txt"
+    f.write_text("max_batch_size { value: 32 }\nnum_batch_threads { value: 8 }\n")
+    cfg = config_from_args([f"--batching_parameters_file={f}"], env={})
+    assert cfg.batching.num_batch_threads == 8
+    assert cfg.executors_for(8) == 1 and cfg.executors_for(4) == 2 and cfg.executors_for(1) == 2
+    cfg = config_from_args([f"--batching_parameters_file={f}", "--executors_per_gpu=3"], env={})
+    assert cfg.executors_for(8) == 3
+    assert config_from_args([], env={}).executors_for(8) == 1
