@@ -7,6 +7,7 @@
 
 #include "kernels/launch.h"
 #include "runtime/engine.h"
+#include "runtime/hip_backend.h"
 
 namespace py = pybind11;
 using namespace kdl;
@@ -319,6 +320,46 @@ PYBIND11_MODULE(_C, m) {
     chk(u8_to_bf16_norm(reinterpret_cast<const uint8_t*>(x), reinterpret_cast<uint16_t*>(y), npix, ldy, S(s)),
         "u8_to_bf16_norm");
   });
+
+  // device backend of the native batch executor (kdl._rt.Executor drives it from a C++ thread)
+  py::class_<HipExecBackend>(m, "HipExecBackend")
+      .def(py::init([](int device, int nslots, size_t item_bytes, int max_batch, int out_cols, uintptr_t copy_stream,
+                       bool timing) {
+             return new HipExecBackend(device, nslots, item_bytes, max_batch, out_cols, S(copy_stream), timing);
+           }),
+           py::arg("device"), py::arg("nslots"), py::arg("item_bytes"), py::arg("max_batch"), py::arg("out_cols"),
+           py::arg("copy_stream") = 0, py::arg("timing") = true)
+      // progs[slot][parity][stage]: Program objects kept alive by the caller
+      .def("add_recipe", [](HipExecBackend& be, int bucket, std::vector<uintptr_t> streams, std::vector<int> wait_for,
+                            py::list progs, std::vector<uintptr_t> dev_in, std::vector<uintptr_t> dev_out) {
+        std::vector<hipStream_t> st;
+        for (auto v : streams) st.push_back(S(v));
+        std::vector<std::vector<std::vector<const Program*>>> pp;
+        for (auto slot : progs) {
+          std::vector<std::vector<const Program*>> ps;
+          for (auto par : slot.cast<py::list>()) {
+            std::vector<const Program*> pk;
+            for (auto prog : par.cast<py::list>()) pk.push_back(&prog.cast<const Program&>());
+            ps.push_back(pk);
+          }
+          pp.push_back(ps);
+        }
+        std::vector<void*> di, dout;
+        for (auto v : dev_in) di.push_back(reinterpret_cast<void*>(v));
+        for (auto v : dev_out) dout.push_back(reinterpret_cast<void*>(v));
+        be.add_recipe(bucket, st, wait_for, pp, di, dout);
+      })
+      .def("api_ptr", [](const HipExecBackend& be) { return reinterpret_cast<uintptr_t>(be.api()); })
+      .def("staging_ptr", [](HipExecBackend& be, int slot) { return reinterpret_cast<uintptr_t>(be.staging(slot)); })
+      // direct use without the executor (tests): issue + complete of one slot
+      .def("run", [](HipExecBackend& be, int slot, int bucket, int n_real) {
+        py::gil_scoped_release nogil;
+        const float* out = nullptr;
+        kdl_device_times t{};
+        if (be.issue(slot, bucket, n_real) != 0 || be.complete(slot, &out, &t) != 0)
+          throw std::runtime_error("HipExecBackend: batch failed");
+        return std::make_tuple(reinterpret_cast<uintptr_t>(out), t.h2d_ms, t.forward_ms, t.d2h_ms);
+      });
 
   py::class_<Program>(m, "Program")
       .def(py::init<>())

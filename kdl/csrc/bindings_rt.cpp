@@ -10,6 +10,7 @@
 #include <sstream>
 
 #include "runtime/batcher.h"
+#include "runtime/executor.h"
 #include "runtime/sstable.h"
 #include "runtime/tfproto.h"
 
@@ -174,6 +175,66 @@ PYBIND11_MODULE(_rt, m) {
         d["padded_items"] = s.padded_items; d["queue_items"] = s.queue_items;
         return d;
       });
+  // ---- native batch executor (executor.h) + the fake device backend used by CPU tests
+  py::class_<ExecGroup>(m, "ExecGroup")
+      .def(py::init<>())
+      .def("healthy", &ExecGroup::healthy);
+  py::class_<FakeBackend>(m, "FakeBackend")
+      .def(py::init<int, size_t, int, int, int64_t, int>(), py::arg("nslots"), py::arg("item_bytes"),
+           py::arg("max_batch"), py::arg("out_cols"), py::arg("latency_us") = 0, py::arg("fail_every") = 0)
+      .def("api_ptr", [](FakeBackend& f) { return reinterpret_cast<uintptr_t>(&f.api); })
+      .def_readonly("issued", &FakeBackend::issued);
+  py::class_<Executor>(m, "Executor")
+      // `batcher`, `group` and the backend behind `backend_ptr` must outlive the executor
+      // (the Python wrapper keeps references to all three)
+      .def(py::init([](DynamicBatcher* b, uintptr_t backend_ptr, ExecGroup* g, const std::string& name, bool eager,
+                       int max_failures, int64_t poll_us, int fail_batches, int64_t delay_us, int trace_ring) {
+             ExecOptions o;
+             o.name = name; o.eager = eager; o.max_failures = max_failures; o.poll_us = poll_us;
+             o.fail_batches = fail_batches; o.delay_us = delay_us; o.trace_ring = trace_ring;
+             return new Executor(b, reinterpret_cast<const kdl_exec_backend*>(backend_ptr), g, o);
+           }),
+           py::arg("batcher"), py::arg("backend_ptr"), py::arg("group"), py::arg("name") = "exec",
+           py::arg("eager") = true, py::arg("max_failures") = 3, py::arg("poll_us") = 100000,
+           py::arg("fail_batches") = 0, py::arg("delay_us") = 0, py::arg("trace_ring") = 256)
+      .def("start", &Executor::start)
+      .def("stop", [](Executor& e) { py::gil_scoped_release nogil; e.stop(); })
+      .def("healthy", &Executor::healthy)
+      .def("running", &Executor::running)
+      .def("stats", [](const Executor& e) {
+        const ExecStats s = e.stats();
+        py::dict d;
+        d["batches"] = s.batches; d["items"] = s.items; d["padded_items"] = s.padded_items;
+        d["failed_batches"] = s.failed_batches; d["healthy"] = s.healthy;
+        py::dict st;
+        py::list le;
+        for (int i = 0; i < N_BUCKETS; ++i) le.append(kBucketsMs[i]);
+        for (int k = 0; k < N_STAGES; ++k) {
+          py::dict h;
+          h["count"] = s.hist[k].count; h["sum_ms"] = s.hist[k].sum_ms;
+          py::list bk;
+          for (int i = 0; i < N_BUCKETS; ++i) bk.append(s.hist[k].buckets[i]);
+          h["buckets"] = bk;
+          st[exec_stage_name(k)] = h;
+        }
+        d["stages"] = st;
+        d["le_ms"] = le;
+        return d;
+      })
+      .def("recent", [](const Executor& e, int n) {
+        py::list out;
+        for (const BatchTrace& t : e.recent(n)) {
+          py::dict d;
+          d["batch_id"] = t.batch_id; d["n_real"] = t.n_real; d["bucket"] = t.bucket; d["slot"] = t.slot;
+          d["status"] = t.status; d["oldest_enqueue_us"] = t.oldest_enqueue_us; d["formed_us"] = t.formed_us;
+          d["copied_us"] = t.copied_us; d["issued_us"] = t.issued_us; d["completed_us"] = t.completed_us;
+          d["finished_us"] = t.finished_us; d["h2d_ms"] = t.h2d_ms; d["forward_ms"] = t.forward_ms;
+          d["d2h_ms"] = t.d2h_ms;
+          out.append(d);
+        }
+        return out;
+      }, py::arg("n") = 64);
+
   m.attr("ST_OK") = int(ST_OK);
   m.attr("ST_DEADLINE") = int(ST_DEADLINE);
   m.attr("ST_SHUTDOWN") = int(ST_SHUTDOWN);

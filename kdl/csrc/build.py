@@ -42,8 +42,9 @@ def _hipcc() -> str:
 
 
 GPU_SOURCES = sorted((HERE / "kernels").glob("*.hip")) + [HERE / "runtime" / "engine.cpp",
+                                                         HERE / "runtime" / "hip_backend.cpp",
                                                          HERE / "bindings_gpu.cpp"]
-RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "tfproto.cpp", "sstable.cpp")] + [
+RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp")] + [
     HERE / "bindings_rt.cpp"]
 HEADERS = sorted(HERE.rglob("*.h"))
 

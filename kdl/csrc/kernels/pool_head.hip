@@ -172,7 +172,9 @@ static int pool_algo(const PoolAddArgs& a) {
 
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
   if (a.C % 8 != 0 || a.dt < 0 || a.dt > 1 || a.B <= 0 || a.OH <= 0 || a.OW <= 0) return hipErrorInvalidValue;
-  if (pool_algo(a) == 2) {
+  // the pixel-per-thread kernel puts B*OH on grid.y (at most 65535): larger batches (e.g. a
+  // server's --max_batch_size above ~885 at Xception block2) take the 1-D row-streaming grid
+  if (pool_algo(a) == 2 || (long)a.B * a.OH > 65535) {
     int seg, rb, nseg, nb;
     pool_rows_plan(a, &seg, &rb, &nseg, &nb);
     const long nblk = ((long)a.B * nb * nseg * (a.C / 8) + 255) / 256;
@@ -186,7 +188,6 @@ hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
 #undef KDL_POOLR
     return hipErrorInvalidValue;
   }
-  if ((long)a.B * a.OH > 65535) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((a.OW * (a.C / 8) + 255) / 256), (unsigned)(a.B * a.OH));
   if (a.dt) hipLaunchKernelGGL(pool_add_kernel<1>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(pool_add_kernel<0>, grid, dim3(256), 0, s, a);

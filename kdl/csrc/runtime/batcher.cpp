@@ -12,10 +12,71 @@ int64_t now_us() {
              std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+CopyPool::CopyPool(int threads) {
+  try {
+    for (int i = 0; i < threads; ++i) workers_.emplace_back([this] { worker(); });
+  } catch (const std::system_error&) {
+    // fewer (or no) helper threads: run() still completes every job on the calling thread
+  }
+}
+
+CopyPool::~CopyPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_work_.notify_all();
+  for (auto& t : workers_) t.join();
+}
+
+void CopyPool::drain(Job& j) {
+  const auto& p = *j.pieces;
+  for (size_t k; (k = j.next.fetch_add(1)) < p.size();) {
+    std::memcpy(p[k].dst, p[k].src, p[k].n);
+    j.done.fetch_add(1, std::memory_order_release);
+  }
+}
+
+void CopyPool::worker() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_work_.wait(lk, [this] { return stop_ || !jobs_.empty(); });
+    if (stop_) return;
+    Job* j = jobs_.front();
+    ++j->users;                                 // the owner keeps the job alive while users > 0
+    lk.unlock();
+    drain(*j);
+    lk.lock();
+    --j->users;
+    if (!jobs_.empty() && jobs_.front() == j) jobs_.pop_front();   // every piece is claimed
+    cv_done_.notify_all();
+  }
+}
+
+void CopyPool::run(const std::vector<Piece>& pieces) {
+  if (pieces.empty()) return;
+  Job j;
+  j.pieces = &pieces;
+  const bool helpers = !workers_.empty() && pieces.size() > 1;
+  if (helpers) {
+    std::lock_guard<std::mutex> lk(mu_);
+    jobs_.push_back(&j);
+  }
+  if (helpers) cv_work_.notify_all();
+  drain(j);
+  if (!helpers) return;
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_done_.wait(lk, [&] { return j.done.load(std::memory_order_acquire) == pieces.size() && j.users == 0; });
+  // unlink before the job leaves this frame (a worker may not have popped it yet)
+  for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
+    if (*it == &j) { jobs_.erase(it); break; }
+}
+
 DynamicBatcher::DynamicBatcher(const BatcherOptions& o) : opt_(o) {
   std::sort(opt_.allowed_batch_sizes.begin(), opt_.allowed_batch_sizes.end());
   if (!opt_.allowed_batch_sizes.empty() && opt_.allowed_batch_sizes.back() != opt_.max_batch_size)
     opt_.allowed_batch_sizes.push_back(opt_.max_batch_size);  // TF-Serving requires last == max
+  if (opt_.copy_threads > 1 && opt_.item_bytes) pool_ = std::make_unique<CopyPool>(opt_.copy_threads - 1);
 }
 
 DynamicBatcher::~DynamicBatcher() { shutdown(); }
@@ -140,6 +201,7 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
       take.push_back(r);
     }
     b->id = next_batch_++;
+    b->formed_us = now_us();
     b->n_real = n;
     b->bucket = bucket_for(n);
     ++st_.batches;
@@ -148,11 +210,10 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
   }
   // payload copies outside the lock (producers stay blocked in wait() on TAKEN). A full
   // Xception batch is 8.6 MB into pinned memory: ~1 ms for one thread, which is most of a
-  // 1.45 ms GPU batch, so large batches are cut into ~1 MiB pieces copied by up to
-  // copy_threads threads (the caller among them)
+  // 1.45 ms GPU batch, so large batches are cut into ~1 MiB pieces copied by the
+  // persistent pool (copy_threads - 1 workers) and the caller; small ones stay on the caller
   if (staging && opt_.item_bytes) {
-    struct Piece { uint8_t* dst; const uint8_t* src; size_t n; };
-    std::vector<Piece> pieces;
+    std::vector<CopyPool::Piece> pieces;
     size_t total = 0;
     constexpr size_t kPiece = size_t(1) << 20;
     for (size_t i = 0; i < take.size(); ++i) {
@@ -162,19 +223,10 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
       for (size_t o = 0; o < n; o += kPiece) pieces.push_back({dst + o, src + o, std::min(kPiece, n - o)});
       total += n;
     }
-    const int nt = (int)std::min<size_t>(std::max(1, opt_.copy_threads), (total + 2 * kPiece - 1) / (2 * kPiece));
-    if (nt <= 1) {
-      for (const auto& p : pieces) std::memcpy(p.dst, p.src, p.n);
+    if (pool_ && total >= 2 * kPiece) {
+      pool_->run(pieces);
     } else {
-      std::atomic<size_t> next{0};
-      auto work = [&]() {
-        for (size_t k; (k = next.fetch_add(1)) < pieces.size();) std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].n);
-      };
-      std::vector<std::thread> th;
-      th.reserve(nt - 1);
-      for (int t = 1; t < nt; ++t) th.emplace_back(work);
-      work();
-      for (auto& t : th) t.join();
+      for (const auto& p : pieces) std::memcpy(p.dst, p.src, p.n);
     }
   }
   {

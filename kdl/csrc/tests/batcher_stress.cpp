@@ -5,7 +5,9 @@
 // (some already expired, some abandoned mid-flight), several consumer threads
 // form batches, copy payloads, "run" them (result row = item's first byte) and
 // finish; a late shutdown races in-flight waits. Every completed request must
-// get back exactly its own rows.
+// get back exactly its own rows. argv[3] = item bytes: large items (e.g. 262144)
+// make every full batch go through the persistent CopyPool from 3 consumers at once,
+// and every byte of each item is checked in the staging copy.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -27,7 +29,8 @@ int main(int argc, char** argv) {
   o.batch_timeout_us = 200;
   o.max_enqueued_batches = 64;
   o.allowed_batch_sizes = {1, 2, 4, 8, 16};
-  o.item_bytes = 64;
+  o.item_bytes = argc > 3 ? size_t(atol(argv[3])) : 64;
+  o.copy_threads = 4;
   o.out_cols = 3;
   DynamicBatcher b(o);
   std::atomic<int> ok{0}, expired{0}, rejected{0}, bad{0};
@@ -42,9 +45,14 @@ int main(int argc, char** argv) {
       while (!stop.load()) {
         Batch bt;
         if (!b.next_batch(staging.data(), 2000, &bt)) continue;
-        for (int i = 0; i < bt.bucket; ++i)
+        for (int i = 0; i < bt.bucket; ++i) {
+          // every byte of a real item must carry its fill value (pooled piece copies)
+          bool whole = true;
+          if (i < bt.n_real)
+            for (size_t q = 1; q < o.item_bytes; q += 4093) whole &= staging[i * o.item_bytes + q] == staging[i * o.item_bytes];
           for (int k = 0; k < o.out_cols; ++k)
-            results[i * o.out_cols + k] = i < bt.n_real ? (float)staging[i * o.item_bytes] + k : -1.f;
+            results[i * o.out_cols + k] = i < bt.n_real ? (whole ? (float)staging[i * o.item_bytes] + k : -7.f) : -1.f;
+        }
         if (rng() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 300));
         b.finish(bt, results.data(), ST_OK);
       }

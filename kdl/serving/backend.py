@@ -1,9 +1,12 @@
 """Servables, signature runners and per-device executors.
 
 Request path: gRPC/REST handler thread -> C++ DynamicBatcher
-(``kdl._rt``; deadline-aware, bucketed) -> one executor thread per device which
-copies the formed batch into pinned staging, H2D, replays the captured
-hipGraph of the bucket, D2H of the logits -> ``finish`` wakes the handlers.
+(``kdl._rt``; deadline-aware, bucketed) -> one executor per device which copies the
+formed batch into pinned staging, H2D, replays the captured hipGraph of the bucket,
+D2H of the logits -> ``finish`` wakes the handlers. On GPUs the executor loop is
+native (``kdl._rt.Executor`` driving ``kdl._C.HipExecBackend`` from a C++ thread:
+no Python and no GIL per batch, per-stage tracing in C++); ``KDL_NATIVE_EXEC=0``
+selects the Python loop below instead.
 
 Backends:
   * ``gpu``: the model family's MI355X engine (``kdl.engine.registry``: fused HIP
@@ -155,6 +158,13 @@ class FaultInjector:
             else:
                 raise ValueError(f"bad KDL_FAULT_INJECT rule {rule!r}")
 
+    def native_args(self, executor: str) -> tuple[int, int]:
+        """(fail_batches, delay_us) for a native executor named ``executor``: the C++ loop
+        applies them itself (kdl/csrc/runtime/executor.cpp)."""
+        fail = next((n for pat, n in self.fail.items() if pat in executor), 0)
+        delay = sum(sec for pat, sec in self.delay.items() if pat in executor)
+        return fail, int(delay * 1e6)
+
     def before_batch(self, executor: str) -> None:
         for pat, sec in self.delay.items():
             if pat in executor:
@@ -184,11 +194,15 @@ class _Executor(threading.Thread):
         self.stop = threading.Event()
         self.ready = threading.Event()
         self.error: BaseException | None = None
-        self.healthy = True
+        self._healthy = True
         self.failures = 0
         self.faults = runner.faults
         bp = runner.cfg.batching
         self.eager = bool(runner.cfg.enable_batching and getattr(bp, "eager_when_idle", True))
+
+    @property
+    def healthy(self) -> bool:
+        return self._healthy
 
     def run(self):
         try:
@@ -197,6 +211,9 @@ class _Executor(threading.Thread):
             self.error = e
             log.exception("executor %s failed to start", self.name)
             self.ready.set()
+            return
+        if getattr(self, "native", None) is not None:
+            self.run_native()
             return
         self.ready.set()
         METRICS.gauge("kdl_executor_healthy", lambda: float(self.healthy), executor=self.name)
@@ -251,7 +268,7 @@ class _Executor(threading.Thread):
         self.failures += 1
         if self.failures < self.max_failures:
             return False
-        self.healthy = False
+        self._healthy = False
         log.error("executor %s: %d consecutive failures, marking device unhealthy and leaving "
                   "the batcher to the other devices", self.name, self.failures)
         if not self.runner.healthy():
@@ -277,10 +294,16 @@ class _Executor(threading.Thread):
 
 
 class GPUExecutor(_Executor):
-    def __init__(self, runner, device: int, engine_kwargs: dict):
-        super().__init__(runner, f"gpu{device}/{runner.sig.name}")
+    def __init__(self, runner, device: int, engine_kwargs: dict, index: int = 0):
+        super().__init__(runner, f"gpu{device}/{runner.sig.name}" + (f"#{index}" if index else ""))
         self.device = device
         self.engine_kwargs = engine_kwargs
+        self.native = None
+        self._busy = (0.0, time.perf_counter())
+
+    @property
+    def healthy(self) -> bool:
+        return self.native.healthy() if self.native is not None else self._healthy
 
     def setup(self):
         from ..engine import registry
@@ -340,10 +363,14 @@ class GPUExecutor(_Executor):
                 e.add_input_slots(self.depth)
         dt = torch.uint8 if in_kind == "u8" else torch.float32
         S = src.input_size
-        self.staging = [torch.zeros((bs[-1], S, S, 3), dtype=dt).pin_memory() for _ in range(self.depth)]
-        self.out = [torch.zeros((bs[-1], src.classes), dtype=torch.float32).pin_memory()
-                    for _ in range(self.depth)]
         self.copy_stream = torch.cuda.Stream(device=self.device)
+        # native executor (default): the C++ loop + HIP backend own the pinned staging; the
+        # split-batch lanes variant exists only on the Python loop
+        want_native = os.environ.get("KDL_NATIVE_EXEC", "1") != "0" and self.lanes is None
+        if not want_native:
+            self.staging = [torch.zeros((bs[-1], S, S, 3), dtype=dt).pin_memory() for _ in range(self.depth)]
+            self.out = [torch.zeros((bs[-1], src.classes), dtype=torch.float32).pin_memory()
+                        for _ in range(self.depth)]
         self.h2d_done = [torch.cuda.Event() for _ in range(self.depth)]
         self.done = [torch.cuda.Event() for _ in range(self.depth)]
         self._rt = _lib.lib()
@@ -356,6 +383,69 @@ class GPUExecutor(_Executor):
                     big.program(bs[-1], capture=cap, slot=slot)
                     big.launch(bs[-1], capture=cap, slot=slot)
         torch.cuda.synchronize(self.device)
+        if want_native:
+            self._build_native(S * S * 3 * (1 if in_kind == "u8" else 4), src.classes)
+
+    def _build_native(self, item_bytes: int, classes: int) -> None:
+        """Hand every bucket's captured graphs to the native executor: a kdl._C.HipExecBackend
+        (pinned staging, H2D -> graphs -> D2H per slot, HIP-event stage times) driven by a
+        kdl._rt.Executor C++ thread that pulls from the signature's batcher."""
+        r, rt = self.runner, _lib.rt()
+        bs = r.buckets
+        be = self._rt.HipExecBackend(self.device, self.depth, item_bytes, bs[-1], classes,
+                                     copy_stream=self.copy_stream.cuda_stream, timing=True)
+        keep = []
+        for bk in bs:
+            if self.pipe is not None and bk == self.pipe.max_batch:
+                e = self.pipe
+                progs = [[e._progs(bk, self.capture, slot, p) for p in (0, 1)] for slot in range(self.depth)]
+                streams, wait_for = [s.cuda_stream for s in e.streams], [int(w) for w in e.wait_for]
+            else:
+                e = self.engine
+                progs = [[[e.program(bk, self.capture, slot)]] * 2 for slot in range(self.depth)]
+                streams, wait_for = [e.stream.cuda_stream], [0]
+            keep.append(progs)                # the backend holds raw Program pointers
+            be.add_recipe(bk, streams, wait_for, progs, [e.inputs[s].data_ptr() for s in range(self.depth)],
+                          [e.slot_logits(s).data_ptr() for s in range(self.depth)])
+        self._native_keep = keep
+        self.backend = be
+        fail, delay_us = self.faults.native_args(self.name)
+        self.native = rt.Executor(r.batcher, be.api_ptr(), r.exec_group, name=self.name, eager=self.eager,
+                                  max_failures=self.max_failures, fail_batches=fail, delay_us=delay_us)
+
+    def run_native(self) -> None:
+        self.native.start()
+        self.ready.set()
+        METRICS.gauge("kdl_executor_healthy", lambda: float(self.healthy), executor=self.name)
+        METRICS.gauge("kdl_gpu_busy_ratio", self._busy_ratio, executor=self.name)
+        METRICS.collector(f"exec/{self.name}", self._native_metrics)
+        self.stop.wait()
+        self.native.stop()
+        METRICS.drop_collector(f"exec/{self.name}")
+
+    def _busy_ratio(self) -> float:
+        """Device utilisation since the previous scrape: summed device forward time of the
+        completed batches over wall time (stage-pipelined batches overlap, so it can exceed 1)."""
+        s = self.native.stats()["stages"]["device_forward"]["sum_ms"] / 1e3
+        now = time.perf_counter()
+        s0, t0 = self._busy
+        self._busy = (s, now)
+        return (s - s0) / max(1e-6, now - t0)
+
+    def _native_metrics(self) -> list[str]:
+        st = self.native.stats()
+        lbl = f'executor="{self.name}"'
+        out = [f"kdl_exec_batches_total{{{lbl}}} {st['batches']}", f"kdl_exec_items_total{{{lbl}}} {st['items']}",
+               f"kdl_exec_padded_items_total{{{lbl}}} {st['padded_items']}",
+               f"kdl_exec_failed_batches_total{{{lbl}}} {st['failed_batches']}"]
+        for stage, h in st["stages"].items():
+            acc = 0
+            for le, c in zip(st["le_ms"], h["buckets"]):
+                acc += c
+                out.append(f'kdl_exec_stage_ms_bucket{{{lbl},stage="{stage}",le="{"+Inf" if le > 1e29 else le}"}} {acc}')
+            out.append(f'kdl_exec_stage_ms_sum{{{lbl},stage="{stage}"}} {h["sum_ms"]:g}')
+            out.append(f'kdl_exec_stage_ms_count{{{lbl},stage="{stage}"}} {h["count"]}')
+        return out
 
     def staging_ptr(self, slot: int = 0) -> int:
         return self.staging[slot].data_ptr()
@@ -421,6 +511,38 @@ class CPUExecutor(_Executor):
         return self.out.data_ptr()
 
 
+class NullExecutor(_Executor):
+    """``--device null``: the native C++ executor loop over kdl._rt.FakeBackend (no device
+    time; result row = {first byte of the item + k}). Everything in front of the device --
+    gRPC, the request codec, the batcher, the executor, the response path -- runs for real,
+    so a closed-loop run against it measures the serving front-end's own ceiling
+    (tools/serve_bench.py --device null)."""
+
+    def __init__(self, runner, index: int = 0):
+        super().__init__(runner, f"null{index}/{runner.sig.name}")
+        self.native = None
+
+    @property
+    def healthy(self) -> bool:
+        return self.native.healthy() if self.native is not None else self._healthy
+
+    def setup(self):
+        r, rt = self.runner, _lib.rt()
+        S = r.source.input_size
+        item = S * S * 3 * (1 if r.sig.input_dtype == P.DT_UINT8 else 4)
+        self.fake = rt.FakeBackend(nslots=2, item_bytes=item, max_batch=r.buckets[-1], out_cols=r.source.classes)
+        fail, delay_us = self.faults.native_args(self.name)
+        self.native = rt.Executor(r.batcher, self.fake.api_ptr(), r.exec_group, name=self.name, eager=self.eager,
+                                  max_failures=self.max_failures, fail_batches=fail, delay_us=delay_us)
+
+    def run_native(self) -> None:
+        self.native.start()
+        self.ready.set()
+        METRICS.gauge("kdl_executor_healthy", lambda: float(self.healthy), executor=self.name)
+        self.stop.wait()
+        self.native.stop()
+
+
 class SignatureRunner:
     """One C++ batcher + the executors serving one signature of one version."""
 
@@ -440,10 +562,14 @@ class SignatureRunner:
                                                 copy_threads=int(os.environ.get("KDL_COPY_THREADS", "4")))
         self.executors: list[_Executor] = []
         self.faults = FaultInjector()
+        self.exec_group = _lib.rt().ExecGroup()     # native executors: last one out shuts the batcher
         if devices:
             for d in devices:
-                for _ in range(cfg.executors_for(len(devices))):
-                    self.executors.append(GPUExecutor(self, d, cfg.engine_kwargs()))
+                for i in range(cfg.executors_for(len(devices))):
+                    self.executors.append(GPUExecutor(self, d, cfg.engine_kwargs(), index=i))
+        elif cfg.device == "null":
+            for i in range(cfg.executors_for(1)):
+                self.executors.append(NullExecutor(self, i))
         else:
             for i in range(cfg.executors_for(1)):
                 self.executors.append(CPUExecutor(self, i))
@@ -535,7 +661,7 @@ class Servable:
 
 
 def pick_devices(cfg: ServerConfig) -> list[int]:
-    if cfg.device == "cpu":
+    if cfg.device in ("cpu", "null"):
         return []
     if torch.cuda.is_available() and _lib.available():
         n = torch.cuda.device_count()

@@ -57,7 +57,7 @@ class ServerConfig:
     file_system_poll_wait_seconds: int = 1
     grpc_max_threads: int = 64
     rest_api_num_threads: int = 16
-    device: str = "auto"          # auto | cpu | gpu
+    device: str = "auto"          # auto | cpu | gpu | null (front-end ceiling: zero-latency fake device)
     gpus: int = 0                 # 0 = all visible
     executors_per_gpu: int = 0    # 0 = derive from batching.num_batch_threads (executors_for)
     synthetic: bool = False       # random-init weights when the repo has no artifact
@@ -95,7 +95,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--file_system_poll_wait_seconds", type=int, default=1)
     ap.add_argument("--grpc_max_threads", type=int, default=64)
     ap.add_argument("--rest_api_num_threads", type=int, default=16)
-    ap.add_argument("--device", choices=["auto", "cpu", "gpu"], default="auto")
+    ap.add_argument("--device", choices=["auto", "cpu", "gpu", "null"], default="auto",
+                    help="null: the native executor over a zero-latency fake device (logits = first "
+                         "input byte + class index) -- measures the serving front-end's own ceiling")
     ap.add_argument("--gpus", type=int, default=0)
     ap.add_argument("--executors_per_gpu", type=int, default=0,
                     help="batch executors per GPU (default: num_batch_threads of the batching "

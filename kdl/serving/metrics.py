@@ -43,6 +43,7 @@ class Metrics:
         self.counters: dict[tuple, float] = defaultdict(float)
         self.hists: dict[tuple, Histogram] = {}
         self.gauges: dict[tuple, callable] = {}
+        self.collectors: dict[str, callable] = {}     # key -> fn() -> list of exposition lines
 
     def inc(self, name: str, value: float = 1.0, **labels) -> None:
         with self._lock:
@@ -58,6 +59,13 @@ class Metrics:
 
     def gauge(self, name: str, fn, **labels) -> None:
         self.gauges[(name, tuple(sorted(labels.items())))] = fn
+
+    def collector(self, key: str, fn) -> None:
+        """Register fn() -> [exposition lines] (native executor histograms), replacing ``key``'s."""
+        self.collectors[key] = fn
+
+    def drop_collector(self, key: str) -> None:
+        self.collectors.pop(key, None)
 
     def hist(self, name: str, **labels) -> Histogram | None:
         return self.hists.get((name, tuple(sorted(labels.items()))))
@@ -82,10 +90,16 @@ class Metrics:
                 out.append(f"{name}_sum{self._lbl(labels)} {h.sum:g}")
                 out.append(f"{name}_count{self._lbl(labels)} {h.n}")
             gauges = list(self.gauges.items())
+            collectors = list(self.collectors.values())
         for (name, labels), fn in sorted(gauges, key=lambda kv: kv[0]):
             try:
                 out.append(f"{name}{self._lbl(labels)} {float(fn()):g}")
             except Exception:  # noqa: BLE001 - a broken gauge must not break scraping
+                pass
+        for fn in collectors:
+            try:
+                out.extend(fn())
+            except Exception:  # noqa: BLE001
                 pass
         return "\n".join(out) + "\n"
 

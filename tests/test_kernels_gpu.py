@@ -254,6 +254,24 @@ def test_pool_add(H, C, with_res):
         assert err <= 2e-2 * ref.abs().max().item(), (kw, err)
 
 
+def test_pool_add_batch_beyond_grid_y_limit():
+    """B * OH > 65535 (a server --max_batch_size of thousands): the pixel-per-thread kernel's
+    grid.y cannot hold it, so the launcher takes the 1-D row-streaming grid instead of failing."""
+    from kdl.models.layers import tf_same_pad
+    gen = torch.Generator().manual_seed(9)
+    B, H, C = 6600, 19, 8
+    OH, pt, _ = tf_same_pad(H, 3, 2)
+    assert B * OH > 65535
+    x = torch.randn(B * H * H * C, generator=gen).to(torch.bfloat16).to(DEV)
+    res = torch.randn(B * OH * OH * C, generator=gen).to(torch.bfloat16).to(DEV)
+    y = torch.full((B * OH * OH * C,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    _lib.lib().pool_add(dict(x=_lib.ptr(x), res=_lib.ptr(res), y=_lib.ptr(y), B=B, H=H, W=H, OH=OH, OW=OH,
+                             C=C, pad_top=pt, pad_left=pt, algo=1), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    ref = pool_add_ref(x, res, B, H, H, OH, OH, C, pt)
+    assert (y.float().view(-1, C) - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("H,cin,C", [(147, 64, 128), (74, 128, 256), (37, 256, 736), (19, 736, 1024)])
 def test_pointwise_pool_epilogue(H, cin, C):
     """Residual 1x1/2 conv with the block's TF-'same' 3x3/2 max-pool fused into its epilogue

@@ -11,7 +11,7 @@ import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "kdl" / "csrc"
-RT = [CSRC / "runtime" / n for n in ("batcher.cpp", "tfproto.cpp", "sstable.cpp")]
+RT = [CSRC / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp")]
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 # TSAN: LLVM's runtime. GCC 11's libtsan does not intercept pthread_cond_clockwait (what
@@ -41,12 +41,33 @@ def test_batcher_under_tsan(tmp_path):
     r = _run(exe, 8, 200, env={"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
     assert r.returncode == 0, r.stdout + r.stderr
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr
+    # 256 KiB items: full batches take the persistent copy pool, from 3 consumers at once
+    r = _run(exe, 6, 60, 262144, env={"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr
 
 
 def test_batcher_under_asan_ubsan(tmp_path):
     exe = _build(tmp_path, "stress_asan", CSRC / "tests" / "batcher_stress.cpp",
                  ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
     r = _run(exe, 8, 200, env={"ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    r = _run(exe, 6, 60, 262144, env={"ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(CLANG is None, reason="needs clang++ (LLVM TSAN runtime)")
+def test_native_executor_under_tsan(tmp_path):
+    exe = _build(tmp_path, "exec_tsan", CSRC / "tests" / "exec_stress.cpp", ["-fsanitize=thread"], cxx=CLANG)
+    r = _run(exe, 8, 120, env={"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr
+
+
+def test_native_executor_under_asan_ubsan(tmp_path):
+    exe = _build(tmp_path, "exec_asan", CSRC / "tests" / "exec_stress.cpp",
+                 ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
+    r = _run(exe, 8, 150, env={"ASAN_OPTIONS": "detect_leaks=1"})
     assert r.returncode == 0, r.stdout + r.stderr
 
 

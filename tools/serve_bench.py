@@ -61,7 +61,9 @@ def main(argv=None) -> int:
     ap.add_argument("--no-eager", action="store_true",
                     help="idle executors wait out the batch timeout (TF-Serving behaviour) instead of "
                          "dispatching whatever is queued")
-    ap.add_argument("--device", default="auto")
+    ap.add_argument("--device", default="auto", help="auto | cpu | gpu | null (zero-latency fake device: "
+                                                    "the serving front-end's own ceiling)")
+    ap.add_argument("--executors-per-gpu", type=int, default=0)
     ap.add_argument("--client-procs", type=int, default=0,
                     help="run the clients in this many spawned processes (0: threads of the server "
                          "process, which then share its GIL with the server's handlers)")
@@ -98,6 +100,7 @@ def main(argv=None) -> int:
         open(os.path.join(base, "1", "synthetic.json"), "w").write('{"seed": 0}')
         sizes = [b for b in (1, 2, 4, 8, 16, 32, 64) if b <= a.max_batch]
         cfg = ServerConfig(port=0, rest_api_port=0, model_base_path=base, device=a.device, gpus=a.gpus,
+                           executors_per_gpu=a.executors_per_gpu,
                            host="127.0.0.1", file_system_poll_wait_seconds=0, grpc_max_threads=max(64, a.clients * 2),
                            batching=BatchingParams(max_batch_size=a.max_batch, batch_timeout_micros=a.timeout_us,
                                                    allowed_batch_sizes=sizes, eager_when_idle=not a.no_eager))
@@ -135,7 +138,8 @@ def main(argv=None) -> int:
     for t in ths:
         t.join()
     span = stop - warm
-    res = {"metric": "closed-loop gRPC serving", "clients": a.clients, "client_procs": a.client_procs,
+    res = {"metric": "closed-loop gRPC serving", "device": a.device, "clients": a.clients,
+           "client_procs": a.client_procs,
            "images_per_request": a.images,
            "signature": a.signature, "requests": len(lat), "images_per_s": round(len(lat) * a.images / span, 1),
            "p50_ms": round(statistics.median(lat) * 1e3, 2),
