@@ -185,16 +185,20 @@ PYBIND11_MODULE(_rt, m) {
       .def("api_ptr", [](FakeBackend& f) { return reinterpret_cast<uintptr_t>(&f.api); })
       .def_readonly("issued", &FakeBackend::issued);
   py::class_<Executor>(m, "Executor")
-      // `batcher`, `group` and the backend behind `backend_ptr` must outlive the executor
-      // (the Python wrapper keeps references to all three)
-      .def(py::init([](DynamicBatcher* b, uintptr_t backend_ptr, ExecGroup* g, const std::string& name, bool eager,
+      // `backend`: any object with api_ptr() -> address of its kdl_exec_backend (kdl._C.HipExecBackend,
+      // FakeBackend). The executor keeps the batcher, the backend and the group alive (keep_alive):
+      // its C++ thread uses all three until stop() joins it in the executor's destructor, whatever
+      // order Python tears objects down in
+      .def(py::init([](DynamicBatcher* b, py::object backend, ExecGroup* g, const std::string& name, bool eager,
                        int max_failures, int64_t poll_us, int fail_batches, int64_t delay_us, int trace_ring) {
              ExecOptions o;
              o.name = name; o.eager = eager; o.max_failures = max_failures; o.poll_us = poll_us;
              o.fail_batches = fail_batches; o.delay_us = delay_us; o.trace_ring = trace_ring;
-             return new Executor(b, reinterpret_cast<const kdl_exec_backend*>(backend_ptr), g, o);
+             const auto ptr = backend.attr("api_ptr")().cast<uintptr_t>();
+             return new Executor(b, reinterpret_cast<const kdl_exec_backend*>(ptr), g, o);
            }),
-           py::arg("batcher"), py::arg("backend_ptr"), py::arg("group"), py::arg("name") = "exec",
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>(),
+           py::arg("batcher"), py::arg("backend"), py::arg("group"), py::arg("name") = "exec",
            py::arg("eager") = true, py::arg("max_failures") = 3, py::arg("poll_us") = 100000,
            py::arg("fail_batches") = 0, py::arg("delay_us") = 0, py::arg("trace_ring") = 256)
       .def("start", &Executor::start)

@@ -9,11 +9,16 @@ the reference lacks (§8.1): JSON errors (400 bad body, 502 fetch/backend errors
 mode that ships uint8 pixels to the ``serving_uint8`` signature (4x fewer bytes).
 
 Env: TF_SERVING_HOST, MODEL_NAME, SIGNATURE, INPUT_KEY, OUTPUT_KEY, LABELS,
-GATEWAY_MODE=compat|uint8, PREDICT_TIMEOUT.
+GATEWAY_MODE=compat|uint8, PREDICT_TIMEOUT, GATEWAY_CHANNELS (gRPC connections to open:
+each gets its own subchannel, so a node running one model-server process per GPU on a
+shared SO_REUSEPORT port -- ``--procs`` -- sees the gateway's requests spread over all
+of them instead of pinned to whichever process accepted a single connection).
 """
 from __future__ import annotations
 
+import itertools
 import os
+import threading
 import urllib.error
 
 import grpc
@@ -37,13 +42,23 @@ class GatewayConfig:
         labels = env.get("LABELS", "")
         self.labels = [s for s in labels.split(",") if s] or list(DEFAULT_LABELS)
         self.timeout = float(env.get("PREDICT_TIMEOUT", "20.0"))
+        self.channels = max(1, int(env.get("GATEWAY_CHANNELS", "1")))
 
 
 def create_app(cfg: GatewayConfig | None = None, channel: grpc.Channel | None = None) -> Flask:
     cfg = cfg or GatewayConfig()
-    channel = channel or grpc.insecure_channel(cfg.server, options=[("grpc.max_send_message_length", -1),
-                                                                     ("grpc.max_receive_message_length", -1)])
-    stub = PredictionStub(channel)
+    opts = [("grpc.max_send_message_length", -1), ("grpc.max_receive_message_length", -1)]
+    if channel is not None:
+        stubs = [PredictionStub(channel)]
+    else:
+        # one connection per channel (a local subchannel pool each), round-robin per request
+        extra = [("grpc.use_local_subchannel_pool", 1)] if cfg.channels > 1 else []
+        stubs = [PredictionStub(grpc.insecure_channel(cfg.server, options=opts + extra)) for _ in range(cfg.channels)]
+    rr, rr_lock = itertools.cycle(stubs), threading.Lock()
+
+    def next_stub():
+        with rr_lock:
+            return next(rr)
     preprocessor = pp.create_preprocessor("xception", target_size=(299, 299))
     app = Flask("clothing-model")
     app.config["kdl_gateway"] = cfg
@@ -55,7 +70,7 @@ def create_app(cfg: GatewayConfig | None = None, channel: grpc.Channel | None = 
 
     def run(X: np.ndarray):
         req = make_request(X, cfg.model_name, cfg.signature, cfg.input_key)
-        return stub.Predict(req, timeout=cfg.timeout)
+        return next_stub().Predict(req, timeout=cfg.timeout)
 
     def fail(code: int, msg: str):
         return jsonify({"error": msg}), code

@@ -410,7 +410,7 @@ class GPUExecutor(_Executor):
         self._native_keep = keep
         self.backend = be
         fail, delay_us = self.faults.native_args(self.name)
-        self.native = rt.Executor(r.batcher, be.api_ptr(), r.exec_group, name=self.name, eager=self.eager,
+        self.native = rt.Executor(r.batcher, be, r.exec_group, name=self.name, eager=self.eager,
                                   max_failures=self.max_failures, fail_batches=fail, delay_us=delay_us)
 
     def run_native(self) -> None:
@@ -532,7 +532,7 @@ class NullExecutor(_Executor):
         item = S * S * 3 * (1 if r.sig.input_dtype == P.DT_UINT8 else 4)
         self.fake = rt.FakeBackend(nslots=2, item_bytes=item, max_batch=r.buckets[-1], out_cols=r.source.classes)
         fail, delay_us = self.faults.native_args(self.name)
-        self.native = rt.Executor(r.batcher, self.fake.api_ptr(), r.exec_group, name=self.name, eager=self.eager,
+        self.native = rt.Executor(r.batcher, self.fake, r.exec_group, name=self.name, eager=self.eager,
                                   max_failures=self.max_failures, fail_batches=fail, delay_us=delay_us)
 
     def run_native(self) -> None:
@@ -637,8 +637,12 @@ class Servable:
         self.runners: dict[str, SignatureRunner] = {}
         self._devices, self._cfg = devices, cfg
         self._lock = threading.Lock()
-        # serving_default is warmed eagerly (readiness = its graphs are captured)
+        # serving_default is warmed eagerly (readiness = its graphs are captured), plus any
+        # --warm_signatures (TF-Serving's warmup analogue: engines built before traffic arrives)
         self.runner("serving_default")
+        for name in cfg.warm_signatures:
+            if name in self.signatures:
+                self.runner(name)
 
     def runner(self, sig_name: str) -> SignatureRunner:
         with self._lock:
@@ -663,6 +667,11 @@ class Servable:
 def pick_devices(cfg: ServerConfig) -> list[int]:
     if cfg.device in ("cpu", "null"):
         return []
+    if cfg.gpu_index >= 0 and (cfg.device == "gpu" or (torch.cuda.device_count() > 0 and _lib.available())):
+        n = torch.cuda.device_count()     # one-process-per-GPU (--procs): this process's GPU only
+        if n == 0:
+            raise RuntimeError("--gpu_index given but no GPU is visible")
+        return [cfg.gpu_index % n]
     if torch.cuda.is_available() and _lib.available():
         n = torch.cuda.device_count()
         k = n if cfg.gpus <= 0 else min(cfg.gpus, n)

@@ -69,6 +69,11 @@ class ServerConfig:
     stages: str = ""              # stage-pipeline cut ("" = the family's default, "none" = off)
     lanes: int = 1                # split-batch hipGraph lanes for the top bucket
     exec_depth: int = 2           # batches in flight per GPU executor
+    # one-process-per-GPU serving (--procs N): N server processes share the gRPC / REST ports
+    # through SO_REUSEPORT; process i serves GPU i % visible GPUs (gpu_index), -1 = all GPUs
+    procs: int = 1
+    gpu_index: int = -1
+    warm_signatures: list[str] = field(default_factory=list)   # built at load, besides serving_default
 
     def executors_for(self, n_devices: int) -> int:
         """Executors per device: --executors_per_gpu when given, else TF-Serving's
@@ -119,6 +124,14 @@ def build_parser() -> argparse.ArgumentParser:
                     help="stage-pipeline cut step (default: the family's; 'none' disables)")
     ap.add_argument("--lanes", type=int, default=None, help="split-batch hipGraph lanes (top bucket)")
     ap.add_argument("--exec_depth", type=int, default=None, help="batches in flight per GPU executor")
+    ap.add_argument("--procs", type=int, default=1,
+                    help="server processes on this node (one per GPU): each binds the same ports with "
+                         "SO_REUSEPORT, so the kernel spreads client connections over them; process i "
+                         "serves GPU i (mod the visible GPUs)")
+    ap.add_argument("--gpu_index", type=int, default=-1, help=argparse.SUPPRESS)   # set by the --procs launcher
+    ap.add_argument("--warm_signatures", default="",
+                    help="comma list of signatures whose engines / graphs are built at model load (like "
+                         "TF-Serving warmup requests); serving_default always is")
     return ap
 
 
@@ -154,4 +167,6 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         labels=labels, host=a.host, dtype=a.dtype, graph=a.graph == "on",
                         stages=a.stages if a.stages is not None else env.get("KDL_STAGES", ""),
                         lanes=a.lanes if a.lanes is not None else int(env.get("KDL_LANES", "1")),
-                        exec_depth=a.exec_depth if a.exec_depth is not None else int(env.get("KDL_EXEC_DEPTH", "2")))
+                        exec_depth=a.exec_depth if a.exec_depth is not None else int(env.get("KDL_EXEC_DEPTH", "2")),
+                        procs=max(1, a.procs), gpu_index=a.gpu_index,
+                        warm_signatures=[s for s in a.warm_signatures.split(",") if s])

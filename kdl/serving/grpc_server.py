@@ -10,6 +10,7 @@ the batcher. Max message size is unlimited like TF-Serving's INT32_MAX.
 from __future__ import annotations
 
 import logging
+import os
 import time
 from concurrent import futures
 
@@ -175,7 +176,10 @@ class Servicer:
 
     # ---------------------------------------------------------------- grpc.health.v1
     def health_check(self, raw: bytes, context) -> bytes:
-        # HealthCheckResponse{status=1 SERVING | 2 NOT_SERVING}
+        # HealthCheckResponse{status=1 SERVING | 2 NOT_SERVING}; the serving process's pid rides in
+        # the initial metadata (which of a node's SO_REUSEPORT processes answered: --procs)
+        if context is not None:
+            context.send_initial_metadata((("kdl-pid", str(os.getpid())),))
         return b"\x08\x01" if self.m.ready() else b"\x08\x02"
 
 
@@ -197,7 +201,7 @@ def signature_def_map(s) -> "P.SignatureDefMap":
     return m
 
 
-def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: int = 64):
+def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: int = 64, reuse_port: bool = False):
     sv = Servicer(manager)
     raw = dict(request_deserializer=None, response_serializer=None)
     pred = grpc.method_handlers_generic_handler("tensorflow.serving.PredictionService", {
@@ -216,7 +220,9 @@ def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: 
     })
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
                          options=[("grpc.max_receive_message_length", -1),
-                                  ("grpc.max_send_message_length", -1)])
+                                  ("grpc.max_send_message_length", -1),
+                                  # --procs: every per-GPU process of the node binds the same port
+                                  ("grpc.so_reuseport", 1 if reuse_port else 0)])
     server.add_generic_rpc_handlers((pred, model, health))
     bound = server.add_insecure_port(f"{host}:{port}")
     return server, bound, sv

@@ -53,7 +53,9 @@ class ModelManager:
 
     def _load(self, v: int) -> None:
         with self._lock:
-            if v in self.servables:
+            # a version already live or being loaded by another thread (the version poller can
+            # fire while the initial load of the same version is still building its engines)
+            if v in self.servables or self.states.get(v, (None, ""))[0] == LOADING:
                 return
             self.states[v] = (LOADING, "")
         t0 = time.perf_counter()

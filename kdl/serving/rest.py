@@ -129,8 +129,19 @@ def make_handler(manager: ModelManager):
     return H
 
 
-def start_rest_server(manager: ModelManager, host: str, port: int):
-    srv = ThreadingHTTPServer((host, port), make_handler(manager))
+class _ReusePortHTTPServer(ThreadingHTTPServer):
+    """SO_REUSEPORT listener: the per-GPU server processes of one node (``--procs``) all bind
+    the same REST port and the kernel spreads connections over them."""
+
+    def server_bind(self):
+        import socket
+        if hasattr(socket, "SO_REUSEPORT"):
+            self.socket.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+        super().server_bind()
+
+
+def start_rest_server(manager: ModelManager, host: str, port: int, reuse_port: bool = False):
+    srv = (_ReusePortHTTPServer if reuse_port else ThreadingHTTPServer)((host, port), make_handler(manager))
     srv.daemon_threads = True
     t = threading.Thread(target=srv.serve_forever, name="rest", daemon=True)
     t.start()

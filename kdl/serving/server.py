@@ -7,9 +7,12 @@ gRPC on --port (8500), REST on --rest_api_port (8501), model from
 from __future__ import annotations
 
 import logging
+import os
 import signal
+import subprocess
 import sys
 import threading
+import time
 
 from .config import ServerConfig, config_from_args
 from .grpc_server import build_grpc_server
@@ -31,18 +34,24 @@ class ModelServer:
     def start(self, block_until_loaded: bool = True) -> "ModelServer":
         cfg = self.cfg
         # serve health/status immediately; Predict returns UNAVAILABLE until loaded
-        self.grpc, self.grpc_port, _ = build_grpc_server(self.manager, cfg.host, cfg.port, cfg.grpc_max_threads)
+        reuse = cfg.gpu_index >= 0           # a child of the --procs launcher: ports are shared
+        self.grpc, self.grpc_port, _ = build_grpc_server(self.manager, cfg.host, cfg.port, cfg.grpc_max_threads,
+                                                         reuse_port=reuse)
         self.grpc.start()
         if cfg.rest_api_port:
-            self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port)
+            self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port, reuse_port=reuse)
             self.rest_port = self.rest.server_address[1]
-        loader = threading.Thread(target=self.manager.load_initial, name="model-loader", daemon=True)
+        def load():
+            try:
+                self.manager.load_initial()
+            finally:
+                self.manager.start_polling()     # after the initial load: never a second loader
+        loader = threading.Thread(target=load, name="model-loader", daemon=True)
         loader.start()
         if block_until_loaded:
             loader.join()
             if not self.manager.ready():
                 raise RuntimeError("model failed to load; see log")
-        self.manager.start_polling()
         log.info("kdl model server: gRPC :%s  REST :%s  model %s from %s", self.grpc_port, self.rest_port,
                  cfg.model_name, cfg.model_base_path)
         return self
@@ -55,10 +64,52 @@ class ModelServer:
         self.manager.close()
 
 
+def launch_procs(argv: list[str], cfg: ServerConfig) -> int:
+    """``--procs N``: one server process per GPU on this node, all on the same gRPC / REST ports
+    (SO_REUSEPORT: the kernel spreads client connections over them). The launcher itself never
+    touches a GPU; it forwards SIGTERM / SIGINT, and when one child dies it stops the others and
+    exits with that child's status, so the pod restarts as a whole (k8s restartPolicy)."""
+    if cfg.port == 0 or cfg.rest_api_port < 0:
+        raise SystemExit("--procs needs fixed ports (every process binds the same one)")
+    base = [a for a in argv if not a.startswith(("--procs", "--gpu_index"))]
+    kids = [subprocess.Popen([sys.executable, "-m", "kdl.serving", *base, "--procs=1", f"--gpu_index={i}"])
+            for i in range(cfg.procs)]
+    log.info("kdl model server: %d processes (pids %s) sharing gRPC :%d / REST :%d", cfg.procs,
+             [k.pid for k in kids], cfg.port, cfg.rest_api_port)
+    stopping = threading.Event()
+
+    def forward(signum, _frame):
+        stopping.set()
+        for k in kids:
+            if k.poll() is None:
+                k.send_signal(signum)
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(sig, forward)
+    rc = 0
+    while True:
+        dead = [k for k in kids if k.poll() is not None]
+        if dead or stopping.is_set():
+            rc = next((k.returncode for k in dead if k.returncode), 0)
+            break
+        time.sleep(0.2)
+    for k in kids:
+        if k.poll() is None:
+            k.terminate()
+    for k in kids:
+        try:
+            k.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            k.kill()
+    return rc
+
+
 def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s",
                         stream=sys.stdout)
+    argv = list(sys.argv[1:] if argv is None else argv)
     cfg = config_from_args(argv)
+    if cfg.procs > 1:
+        return launch_procs(argv, cfg)
     srv = ModelServer(cfg).start(block_until_loaded=False)
     done = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):

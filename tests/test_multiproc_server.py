@@ -1,0 +1,101 @@
+"""One server process per GPU (``python -m kdl.serving --procs N``), CPU rehearsal.
+
+Two server processes (null device: the real gRPC front-end, request codec, batcher and
+native executor over a zero-latency fake device) bind the same gRPC port through
+SO_REUSEPORT; independent client connections are spread over both processes by the
+kernel, every Predict answers correctly whichever process took it, and SIGTERM to the
+launcher stops the whole group. This is the scale-out that replaces the reference's
+Deployment replicas behind a ClusterIP Service (tf-serving-clothing-model-deployment.yaml:8,
+tf-serving-clothing-model-service.yaml:1-14) inside one pod.
+"""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import grpc
+import numpy as np
+import pytest
+
+from kdl.gateway.client import PredictionStub, make_request
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _health(target):
+    ch = grpc.insecure_channel(target, options=[("grpc.use_local_subchannel_pool", 1)])
+    call = ch.unary_unary("/grpc.health.v1.Health/Check")
+    try:
+        resp, c = call.with_call(b"", timeout=5)
+        md = dict(c.initial_metadata())
+        return resp, md.get("kdl-pid")
+    finally:
+        ch.close()
+
+
+@pytest.fixture()
+def two_procs(tmp_path):
+    base = tmp_path / "clothing-model"
+    (base / "1").mkdir(parents=True)
+    (base / "1" / "synthetic.json").write_text('{"seed": 0}')
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    p = subprocess.Popen([sys.executable, "-m", "kdl.serving", "--procs=2", f"--port={port}", "--rest_api_port=0",
+                          f"--model_base_path={base}", "--device=null", "--host=127.0.0.1",
+                          "--allowed_batch_sizes=1,2,4,8"], cwd=str(ROOT), env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+    target = f"127.0.0.1:{port}"
+    try:
+        deadline = time.time() + 240
+        pids = set()
+        while time.time() < deadline and len(pids) < 2:     # both processes up and SERVING
+            try:
+                resp, pid = _health(target)
+                if resp == b"\x08\x01":
+                    pids.add(pid)
+            except grpc.RpcError:
+                pass
+            time.sleep(0.2)
+        assert p.poll() is None, "launcher exited"
+        yield p, target
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+
+
+def test_connections_spread_over_both_processes_and_predict_is_right(two_procs):
+    p, target = two_procs
+    pids = {_health(target)[1] for _ in range(40)}
+    assert len(pids) == 2, pids
+    rng = np.random.default_rng(0)
+    for k in range(12):
+        ch = grpc.insecure_channel(target, options=[("grpc.use_local_subchannel_pool", 1),
+                                                    ("grpc.max_send_message_length", -1)])
+        u8 = rng.integers(0, 200, (3, 299, 299, 3), dtype=np.uint8)
+        r = PredictionStub(ch).Predict(make_request(u8, signature="serving_uint8", input_key="images"), timeout=30)
+        got = np.asarray(r.outputs["dense_7"].float_val, np.float32).reshape(3, 10)
+        # the null device answers {first byte of the image + class index}
+        want = u8[:, 0, 0, 0:1].astype(np.float32) + np.arange(10, dtype=np.float32)[None]
+        assert np.array_equal(got, want)
+        ch.close()
+
+
+def test_sigterm_stops_every_process(two_procs):
+    p, target = two_procs
+    os.kill(p.pid, signal.SIGTERM)
+    assert p.wait(timeout=60) == 0
+    with pytest.raises(grpc.RpcError):
+        _health(target)

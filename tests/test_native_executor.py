@@ -55,7 +55,7 @@ def test_two_executors_serve_every_request_with_batches_in_flight():
     b = _batcher()
     g = rt.ExecGroup()
     fakes = [rt.FakeBackend(nslots=2, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, latency_us=300) for _ in range(2)]
-    exs = [rt.Executor(b, f.api_ptr(), g, name=f"fake{i}") for i, f in enumerate(fakes)]
+    exs = [rt.Executor(b, f, g, name=f"fake{i}") for i, f in enumerate(fakes)]
     for e in exs:
         e.start()
     errors, results = _run_clients(b)
@@ -83,8 +83,8 @@ def test_failing_device_is_isolated_and_the_other_serves_everything():
     g = rt.ExecGroup()
     good = rt.FakeBackend(nslots=2, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, latency_us=100)
     bad = rt.FakeBackend(nslots=2, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, latency_us=100, fail_every=1)
-    e_bad = rt.Executor(b, bad.api_ptr(), g, name="bad", max_failures=2)
-    e_good = rt.Executor(b, good.api_ptr(), g, name="good")
+    e_bad = rt.Executor(b, bad, g, name="bad", max_failures=2)
+    e_good = rt.Executor(b, good, g, name="good")
     e_bad.start()
     time.sleep(0.05)
     e_good.start()
@@ -103,7 +103,7 @@ def test_last_executor_giving_up_shuts_the_batcher_so_waiters_do_not_hang():
     b = _batcher()
     g = rt.ExecGroup()
     bad = rt.FakeBackend(nslots=2, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, fail_every=1)
-    e = rt.Executor(b, bad.api_ptr(), g, name="bad", max_failures=1)
+    e = rt.Executor(b, bad, g, name="bad", max_failures=1)
     e.start()
     errors, results = _run_clients(b, n_threads=3, n_req=10)
     e.stop()
@@ -116,7 +116,7 @@ def test_injected_fault_then_recovery_and_trace_statuses():
     b = _batcher()
     g = rt.ExecGroup()
     f = rt.FakeBackend(nslots=3, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, latency_us=50)
-    e = rt.Executor(b, f.api_ptr(), g, name="inj", fail_batches=1, delay_us=100)
+    e = rt.Executor(b, f, g, name="inj", fail_batches=1, delay_us=100)
     e.start()
     errors, results = _run_clients(b, n_threads=2, n_req=20)
     e.stop()
@@ -131,7 +131,7 @@ def test_stop_drains_in_flight_batches(nslots):
     b = _batcher()
     g = rt.ExecGroup()
     f = rt.FakeBackend(nslots=nslots, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, latency_us=2000)
-    e = rt.Executor(b, f.api_ptr(), g, name="drain")
+    e = rt.Executor(b, f, g, name="drain")
     e.start()
     errors, results = [], []
     th = threading.Thread(target=_client, args=(b, 1, 10, errors, results))

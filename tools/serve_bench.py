@@ -22,7 +22,7 @@ import grpc  # noqa: E402
 import numpy as np  # noqa: E402
 
 
-def _client_proc(conn, threads: int, req: bytes, seconds: float, warm_s: float) -> None:
+def _client_proc(conn, threads: int, req: bytes, seconds: float, warm_s: float) -> None:  # noqa: C901
     """Client worker process (spawned BEFORE the server initialises the GPU): receives
     the target, runs `threads` closed-loop clients, sends back the post-warm-up latencies."""
     target = conn.recv()
@@ -31,7 +31,8 @@ def _client_proc(conn, threads: int, req: bytes, seconds: float, warm_s: float) 
     stop, warm = t_start + seconds, t_start + warm_s
 
     def client():
-        ch = grpc.insecure_channel(target, options=[("grpc.max_send_message_length", -1)])
+        ch = grpc.insecure_channel(target, options=[("grpc.max_send_message_length", -1),
+                                                    ("grpc.use_local_subchannel_pool", 1)])
         call = ch.unary_unary("/tensorflow.serving.PredictionService/Predict")
         while time.perf_counter() < stop:
             t0 = time.perf_counter()
@@ -46,6 +47,44 @@ def _client_proc(conn, threads: int, req: bytes, seconds: float, warm_s: float) 
     for t in ths:
         t.join()
     conn.send(lat)
+
+
+def _launch_procs(a):
+    """`python -m kdl.serving --procs N` on a fixed port, waited until every process answers."""
+    import socket
+    import subprocess
+    import tempfile
+    base = os.path.join(tempfile.mkdtemp(), "clothing-model")
+    os.makedirs(os.path.join(base, "1"))
+    open(os.path.join(base, "1", "synthetic.json"), "w").write('{"seed": 0}')
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    sizes = ",".join(str(b) for b in (1, 2, 4, 8, 16, 32, 64) if b <= a.max_batch)
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+    cmd = [sys.executable, "-m", "kdl.serving", f"--procs={a.procs}", f"--port={port}", "--rest_api_port=0",
+           f"--model_base_path={base}", f"--device={a.device}", "--host=127.0.0.1", f"--allowed_batch_sizes={sizes}",
+           f"--batch_timeout_micros={a.timeout_us}", f"--grpc_max_threads={max(64, a.clients * 2)}",
+           f"--warm_signatures={a.signature}"]
+    if a.executors_per_gpu:
+        cmd.append(f"--executors_per_gpu={a.executors_per_gpu}")
+    p = subprocess.Popen(cmd, cwd=root, env=dict(os.environ, PYTHONPATH=root), stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, start_new_session=True)
+    target = f"127.0.0.1:{port}"
+    seen, t_end = set(), time.time() + 600
+    while len(seen) < a.procs and time.time() < t_end and p.poll() is None:
+        ch = grpc.insecure_channel(target, options=[("grpc.use_local_subchannel_pool", 1)])
+        try:
+            resp, call = ch.unary_unary("/grpc.health.v1.Health/Check").with_call(b"", timeout=5)
+            if resp == b"\x08\x01":
+                seen.add(dict(call.initial_metadata()).get("kdl-pid"))
+        except grpc.RpcError:
+            time.sleep(0.5)
+        finally:
+            ch.close()
+    if len(seen) < a.procs:
+        raise SystemExit(f"only {len(seen)} of {a.procs} server processes came up")
+    return p, target
 
 
 def main(argv=None) -> int:
@@ -64,6 +103,10 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto", help="auto | cpu | gpu | null (zero-latency fake device: "
                                                     "the serving front-end's own ceiling)")
     ap.add_argument("--executors-per-gpu", type=int, default=0)
+    ap.add_argument("--procs", type=int, default=0,
+                    help="serve from `python -m kdl.serving --procs N` (N processes sharing the port via "
+                         "SO_REUSEPORT, one per GPU mod the visible GPUs) instead of an in-process server; "
+                         "every client opens its own connection")
     ap.add_argument("--client-procs", type=int, default=0,
                     help="run the clients in this many spawned processes (0: threads of the server "
                          "process, which then share its GIL with the server's handlers)")
@@ -89,7 +132,10 @@ def main(argv=None) -> int:
             procs.append((pr, parent))
     from kdl.gateway.client import PredictionStub, make_request
     srv = None
+    launcher = None
     target = a.target
+    if target is None and a.procs:
+        launcher, target = _launch_procs(a)
     if target is None:
         import tempfile
 
@@ -123,7 +169,8 @@ def main(argv=None) -> int:
             pr.join()
 
     def client():
-        ch = grpc.insecure_channel(target, options=[("grpc.max_send_message_length", -1)])
+        ch = grpc.insecure_channel(target, options=[("grpc.max_send_message_length", -1),
+                                                    ("grpc.use_local_subchannel_pool", 1)])
         call = ch.unary_unary("/tensorflow.serving.PredictionService/Predict")
         while time.perf_counter() < stop:
             t0 = time.perf_counter()
@@ -148,6 +195,11 @@ def main(argv=None) -> int:
         st = srv.manager.get("clothing-model").runner(a.signature).batcher.stats()
         res["mean_batch"] = round(st["items"] / max(1, st["batches"]), 2)
         srv.stop(0)
+    if launcher is not None:
+        import signal
+        res["procs"] = a.procs
+        os.killpg(launcher.pid, signal.SIGTERM)
+        launcher.wait(timeout=60)
     print(json.dumps(res), flush=True)
     return 0
 
