@@ -61,6 +61,31 @@ constexpr int SEPW_CFG_BASE = 120;
 hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_ws_fits(int cfg, int W);
+
+// Chained launch of fused separable convs of one geometry (the Xception middle flow): ONE
+// launch runs `nlayers` layers; its workgroups take (layer, tile) tickets from an atomic queue
+// in layer-major order and a tile of layer l starts once the three M tiles of layer l-1 whose
+// rows its 3x3 halo reads are published (write-through stores + per-(layer, M tile) counters,
+// agent-scope acquire). Deadlock-free at any residency: a ticket's dependencies were taken
+// earlier, by workgroups that are running. `sync` must be zeroed before every launch.
+struct ChainArgs {
+  static constexpr int MAXL = 32;
+  ConvGemmArgs g;               // shared geometry / flags (its pointers unused)
+  const uint16_t* x[MAXL];      // per layer, in kernel arguments (uniform scalar loads)
+  const uint16_t* wp[MAXL];
+  const uint16_t* dwk[MAXL];
+  const uint16_t* res[MAXL];
+  uint16_t* y[MAXL];
+  const float* bias[MAXL];
+  unsigned relu_in;             // bit l: ReLU on layer l's input
+  unsigned relu_out;            // bit l: ReLU before layer l's residual add (ConvGemmArgs.relu_out 1)
+  int nlayers;
+  int* sync;                    // [0] queue head, [1] error (spin gave up), [4 + l * nM + mi] done N tiles
+  int nM, nN;                   // tiles per layer (host-computed from the config's tile)
+  int spin_limit;               // dependency polls before giving up (error word set, result garbage)
+};
+hipError_t sepconv_chain(int cfg, const ChainArgs& c, hipStream_t s);
+int sepconv_chain_tiles(int cfg, int M, int NF, int* nM, int* nN);
 // cfg >= C3_CFG_BASE: 3x3 'valid' conv over 2-D tiles with an LDS halo patch (MODE_CONV, cin 32 only,
 // conv3x3_2d.hip: Xception block1_conv2).
 constexpr int C3_CFG_BASE = 208;

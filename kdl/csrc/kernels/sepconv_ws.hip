@@ -28,6 +28,8 @@
 #include "launch.h"
 #include "epilogue.h"
 
+#include <algorithm>
+
 namespace kdl {
 
 // zeros for band slots beyond the staged pixels (K <= 8192); one per translation unit
@@ -43,8 +45,20 @@ __device__ __forceinline__ void ws_wait_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU>
-__global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
+// LDS bytes of one workgroup of the configuration (the tile body's layout)
+template <int FM, int FN, int STAGES, int XB>
+struct WsSmem {
+  static constexpr int RING = STAGES * (XB + 1) * 1024;
+  static constexpr int PIPE = RING + 2 * FM * 1024;
+  static constexpr int CTILE = 16 * FM * (64 * FN * 2 + 16);
+  static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
+};
+
+// One BM x BN output tile of a fused separable conv: the whole body of sepconv_ws_kernel,
+// also run per work item by the persistent chain kernel below (CHAIN: write-through sc1
+// stores of the output and the caller publishes the tile; residual read after its acquire).
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, bool CHAIN>
+__device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, uint8_t* smem) {
   constexpr int NT = 512;
   constexpr int BM = 16 * FM, BN = 64 * FN;
   constexpr int AF = FM;
@@ -63,17 +77,13 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   // the LCB + FN loads of step t-1 may still be in flight
   constexpr int WC = LCB + FN;
   static_assert(FM % 2 == 0 && STAGES >= 5, "layout / pipeline depth");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+  static_assert(SMEM == WsSmem<FM, FN, STAGES, XB>::BYTES, "LDS map");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool consumer = wave < 4;
   const int W = a.W, H = a.H;
   const long NPIX = (long)a.B * H * W;
-  const int nN = (a.NF * 16) / BN;
-  const int nM = (a.M + BM - 1) / BM;
-  const int wg = xcd_remap(blockIdx.x, nM * nN);
-  const int mi = wg / nN, ni = wg % nN;
   const int m0 = mi * BM, n0 = ni * BN;
   const int KT = a.K >> 5;
   const int KTE = (KT + 1) & ~1;                 // even step count (unroll by 2)
@@ -328,11 +338,103 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   }
   __syncthreads();
   constexpr int CPR = BN / 8;
-  for (int c = tid; c < BM * CPR; c += NT) {
-    const int r = c / CPR, cc = c - r * CPR;
-    const int m = m0 + r, n = n0 + cc * 8;
-    if (m < a.M && n < a.nstore) epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+  if constexpr (CHAIN) {
+    // write-through (sc1) 16-B stores: the tile is handed to other workgroups inside the launch
+    // (Guideline 16 R1: no release fence; the caller drains and publishes)
+    const __amdgpu_buffer_rsrc_t yr =
+        __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)min((long)a.M * a.ldy * 2, 0x7fffffffL), 0x00020000);
+    for (int c = tid; c < BM * CPR; c += NT) {
+      const int r = c / CPR, cc = c - r * CPR;
+      const int m = m0 + r, n = n0 + cc * 8;
+      if (m < a.M && n < a.nstore) {
+        u32x4 v = *(const u32x4*)(smem + r * CS + cc * 16);
+        if (a.res) {
+          const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
+#pragma unroll
+          for (int d = 0; d < 4; ++d) v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
+        }
+        if (a.relu_out == 2) {
+#pragma unroll
+          for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, (int)(((long)m * a.ldy + n) * 2), 0, 16);
+      }
+    }
+  } else {
+    for (int c = tid; c < BM * CPR; c += NT) {
+      const int r = c / CPR, cc = c - r * CPR;
+      const int m = m0 + r, n = n0 + cc * 8;
+      if (m < a.M && n < a.nstore) epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+    }
   }
+}
+
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU>
+__global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[WsSmem<FM, FN, STAGES, XB>::BYTES];
+  constexpr int BM = 16 * FM, BN = 64 * FN;
+  const int nN = (a.NF * 16) / BN;
+  const int nM = (a.M + BM - 1) / BM;
+  const int wg = xcd_remap(blockIdx.x, nM * nN);
+  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, false>(a, wg / nN, wg % nN, smem);
+}
+
+// ---------------------------------------------------------------------------
+// Chained launch (launch.h ChainArgs): the middle flow's sepconv layers in ONE launch of
+// nlayers * tiles workgroups. Each workgroup takes a ticket from an atomic queue (NOT its
+// blockIdx: the dispatcher's order is not a promise) and tickets are layer-major, so every
+// tile a ticket waits for was taken by a workgroup that is already running: no deadlock at
+// any residency, with other kernels or executors sharing the GPU. Per ticket: wait for the
+// previous layer's M tiles mi-1..mi+1 (relaxed agent polls of their counters, s_sleep,
+// bounded) -> ONE agent acquire -> the ws tile (write-through output) -> every wave drains its
+// stores -> one lane counts the tile (MI355X_MICROARCH.md § visibility, Guideline 16 R1).
+// Saves per layer the launch, the grid fill and drain and the kernel boundary. (A persistent
+// loop over tickets was tried first: live ranges across its iterations made the 6x6 tile
+// spill.)
+template <int FM, int FN, int STAGES, int XB>
+__global__ __launch_bounds__(512) void sepconv_chain_kernel(ChainArgs c) {
+  // ONE __shared__ array (a second LDS object can make hipcc wait vmcnt(0) before every
+  // k-step's first LDS read: cdna_hip_programming.md §5 trap (a)); the ticket word sits past the map
+  constexpr int BYTES = WsSmem<FM, FN, STAGES, XB>::BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[BYTES + 16];
+  int* const s_item = (int*)(smem + BYTES);
+  const int tid = threadIdx.x;
+  const int tiles = c.nM * c.nN;
+  int* const cnt = c.sync + 4;
+  if (tid == 0) *s_item = __hip_atomic_fetch_add(c.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int item = __builtin_amdgcn_readfirstlane(*s_item);
+  const int layer = item / tiles, t = item - layer * tiles;
+  const int mi = t / c.nN, ni = t - mi * c.nN;
+  if (tid == 0) {
+    if (layer > 0) {
+      const int* dep = cnt + (layer - 1) * c.nM;
+      for (int d = max(0, mi - 1); d <= min(c.nM - 1, mi + 1); ++d) {
+        int spins = 0;
+        while (__hip_atomic_load(dep + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c.nN) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > c.spin_limit) {
+            __hip_atomic_store(c.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();                              // every wave loads only after the acquire
+  ConvGemmArgs a = c.g;
+  a.x = c.x[layer]; a.wp = c.wp[layer]; a.dwk = c.dwk[layer]; a.res = c.res[layer];
+  a.y = c.y[layer]; a.bias = c.bias[layer]; a.relu_in = (c.relu_in >> layer) & 1;
+  a.relu_out = (c.relu_out >> layer) & 1;
+  if (a.relu_in)
+    ws_tile<FM, FN, STAGES, XB, false, true, true, true>(a, mi, ni, smem);
+  else
+    ws_tile<FM, FN, STAGES, XB, false, true, false, true>(a, mi, ni, smem);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // EVERY storing wave drains its sc1 stores
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(cnt + layer * c.nM + mi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // (FM, FN, STAGES, XB = band KiB): tile BM = 16*FM, BN = 64*FN; LDS = STAGES*(XB+1) KiB + 2FM KiB
@@ -412,6 +514,49 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)
 #undef KDL_SWCASE
+  }
+  return hipGetLastError();
+}
+
+// chain configurations: the K-rotated ws ids (23 .. 26 = tiles of ids 0, 2, 3, 5)
+#define KDL_CHAIN_CONFIGS(X) \
+  X(23, 6, 6, 5, 9)          \
+  X(24, 6, 6, 5, 11)         \
+  X(26, 4, 6, 5, 8)
+
+static int chain_bm(int cfg) {
+  switch (cfg) {
+#define KDL_CHBM(id, fm, fn, st, xb) case id: return 16 * fm;
+    KDL_CHAIN_CONFIGS(KDL_CHBM)
+#undef KDL_CHBM
+    default: return 0;
+  }
+}
+
+int sepconv_chain_tiles(int cfg, int M, int NF, int* nM, int* nN) {
+  switch (cfg) {
+#define KDL_CHTILES(id, fm, fn, st, xb) \
+  case id: *nM = (M + 16 * fm - 1) / (16 * fm); *nN = (NF * 16) / (64 * fn); return (NF * 16) % (64 * fn) ? -1 : 0;
+    KDL_CHAIN_CONFIGS(KDL_CHTILES)
+#undef KDL_CHTILES
+    default: return -1;
+  }
+}
+
+hipError_t sepconv_chain(int cfg, const ChainArgs& c, hipStream_t s) {
+  const ConvGemmArgs& g = c.g;
+  int nM = 0, nN = 0;
+  if (sepconv_chain_tiles(cfg, g.M, g.NF, &nM, &nN) != 0 || nM != c.nM || nN != c.nN || c.nlayers < 1 ||
+      c.nlayers > ChainArgs::MAXL || !c.sync || !sepconv_ws_fits(cfg, g.W) || g.K % 32 != 0 || g.K > 8192 || g.OH != g.H ||
+      g.OW != g.W || g.M <= 0 || c.spin_limit < 1 || chain_bm(cfg) < g.W + 1)   // halo within mi +- 1
+    return hipErrorInvalidValue;
+  const int grid = nM * nN * c.nlayers;        // one workgroup per ticket
+  switch (cfg) {
+#define KDL_CHCASE(id, fm, fn, st, xb) \
+  case id: hipLaunchKernelGGL((sepconv_chain_kernel<fm, fn, st, xb>), dim3(grid), dim3(512), 0, s, c); break;
+    KDL_CHAIN_CONFIGS(KDL_CHCASE)
+#undef KDL_CHCASE
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

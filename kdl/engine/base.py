@@ -94,10 +94,9 @@ class EngineBase:
         prog = _lib.lib().Program()
         self._slot = slot
         try:
-            for step in self.steps:
-                self._emit_marked(prog, step, b)
+            self._emit_steps(prog, self.steps, [{}] * len(self.steps), b)
         finally:
-            self._slot = 0
+            self._slot, self._remap = 0, {}
         if capture:
             with torch.cuda.device(self.device):
                 prog.capture(int(self.stream.cuda_stream))
@@ -128,9 +127,7 @@ class EngineBase:
         prog = _lib.lib().Program()
         self._slot = slot
         try:
-            for step, m in zip(self.steps[lo:hi], maps):
-                self._remap = m
-                self._emit_marked(prog, step, b)
+            self._emit_steps(prog, self.steps[lo:hi], maps, b)
         finally:
             self._slot, self._remap = 0, {}
         if capture:
@@ -138,6 +135,28 @@ class EngineBase:
                 prog.capture(int(self.stream.cuda_stream))
         self.programs[key] = prog
         return prog
+
+    def _emit_steps(self, prog, steps: list[Step], maps: list[dict], b: int) -> None:
+        """Emit a run of steps (each with its buffer remap). Runs that ``_chain_end`` groups
+        become ONE chained launch (``_emit_chain``); a program range never chains across its
+        ends, so a stage cut (stages.py) always falls between launches."""
+        i = 0
+        while i < len(steps):
+            j = self._chain_end(steps, i)
+            if j - i >= 2:
+                self._emit_chain(prog, steps[i:j], maps[i:j], b)
+                i = j
+                continue
+            self._remap = maps[i]
+            self._emit_marked(prog, steps[i], b)
+            i += 1
+
+    def _chain_end(self, steps: list[Step], i: int) -> int:
+        """End (exclusive) of the chainable run starting at steps[i]; <= i + 1: no chain."""
+        return i + 1
+
+    def _emit_chain(self, prog, steps: list[Step], maps: list[dict], b: int) -> None:
+        raise NotImplementedError
 
     def _emit_marked(self, prog, step: Step, b: int) -> None:
         """Emit one step and carry its graph-concurrency marks onto its ops: extra

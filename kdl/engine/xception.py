@@ -7,6 +7,10 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
     conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
     conv_gemm MODE_PW    residual 1x1/2 convs + BN (KDL_POOLFUSE=1: with the block's
                          3x3/2 max-pool of the main branch added in the epilogue, "convpool")
+    seppool              an entry block's last SeparableConv2D + its 3x3/2 max-pool + the
+                         residual add in ONE kernel (sepconv_2dwp_kernel, "seppool" steps;
+                         KDL_SEP_POOL=0 restores conv + pool_add); where no pooled config
+                         fits (wide K x N weights), pool_add:
     pool_add             TF-'same' 3x3/2 max-pool + residual add
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
 
@@ -26,10 +30,13 @@ import torch
 from ..models import xception as X
 from ..models.layers import tf_same_pad
 from ..ops import _lib
-from ..ops.conv import (MODE_CONV, MODE_DW, MODE_PW, ConvGemmLayer, Geometry,
-                        conv_weights_nk)
+from ..ops.conv import (CHAIN_CONFIGS, MODE_CONV, MODE_DW, MODE_PW, SEPW_BASE, ConvGemmLayer, Geometry,
+                        cfg_tile, config_applicable, conv_weights_nk, pool_configs)
 from ..ops.pack import bn_scale_shift, pack_fragments, round_up, rowrun_weights
 from .base import EngineBase, Step
+
+
+CHAIN_MAX_LAYERS = 32          # launch.h ChainArgs::MAXL
 
 
 class XceptionEngine(EngineBase):
@@ -52,6 +59,15 @@ class XceptionEngine(EngineBase):
         # dependent 16-B pool reads per output chunk are latency-bound inside the GEMM's store
         # loop, so the fused launch (80.8 us at block2) costs what conv + pool_add did (82.6)
         self.poolfuse = os.environ.get("KDL_POOLFUSE", "0") == "1" and not self.branches
+        # KDL_SEP_POOL (default on): the block's last separable conv writes maxpool + residual
+        # directly (sepconv_2dwp_kernel); bit-identical to conv + pool_add
+        self.seppool = os.environ.get("KDL_SEP_POOL", "1") != "0" and not self.poolfuse
+        self.seppool_cfg = int(os.environ.get("KDL_SEP_POOL_CFG", "0"))
+        # KDL_CHAIN=<cfg> (0 = off): each run of same-geometry separable convs inside one
+        # program (the middle flow: blocks 5-12 + block13_sepconv1, split only at a stage cut)
+        # becomes ONE chained launch (sepconv_chain_kernel, launch.h ChainArgs) with that ws tile
+        self.chain_cfg = int(os.environ.get("KDL_CHAIN", "0"))
+        self._chain_sync: dict[tuple, torch.Tensor] = {}
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
@@ -106,14 +122,27 @@ class XceptionEngine(EngineBase):
                                            extra=dict(branch=self.branches)))
                     self.shapes[rname] = (oh, oh, lay.ldy)
                 y = cur
-                for op in blk.main:
+                _, pt, _ = tf_same_pad(H, 3, 2)
+                out = f"block{bi + 1}_out"
+                pooled = False
+                for k, op in enumerate(blk.main):
                     lay = self._sep(p, op, dev)
                     dst = f"{op.name}_out"
+                    pcfgs = pool_configs(lay.K, lay.n, pt) if self.seppool and k == len(blk.main) - 1 else []
+                    if pcfgs and rlay.ldy == lay.ldy:
+                        # separable conv + block max-pool + residual in one kernel: no full-res output
+                        cfg = self.seppool_cfg if self.seppool_cfg in pcfgs else pcfgs[0]
+                        self.steps.append(Step("seppool", op.name, lay, y, out, res=rname, geom=(H, H, oh, oh),
+                                               extra=dict(pad=pt, cfg=cfg)))
+                        self.shapes[out] = (oh, oh, lay.ldy)
+                        pooled = True
+                        break
                     self.steps.append(Step("conv", op.name, lay, y, dst, geom=(H, H, H, H)))
                     self.shapes[dst] = (H, H, lay.ldy)
                     y = dst
-                _, pt, _ = tf_same_pad(H, 3, 2)
-                out = f"block{bi + 1}_out"
+                if pooled:
+                    cur, H = out, oh
+                    continue
                 C = self.shapes[y][2]
                 if self.poolfuse:
                     # residual conv of the block input, + maxpool(main branch) in its epilogue,
@@ -166,7 +195,7 @@ class XceptionEngine(EngineBase):
                 if b:
                     uses[b] = uses.get(b, 0) + 1
         for a, b in zip(self.steps, self.steps[1:]):
-            if (a.kind == "conv" and b.kind == "conv" and b.src == a.dst and uses.get(a.dst) == 1
+            if (a.kind == "conv" and b.kind in ("conv", "seppool") and b.src == a.dst and uses.get(a.dst) == 1
                     and a.res is None and a.layer.relu_out == 0 and b.layer.mode == MODE_DW and b.layer.relu_in):
                 a.layer.relu_out, b.layer.relu_in = 1, False
 
@@ -231,7 +260,7 @@ class XceptionEngine(EngineBase):
                                           bias=_lib.ptr(self.stem_bias), y=self._ptr(step.dst),
                                           B=b, H=H, W=W, OH=OH, OW=OW, ldy=32,
                                           in_kind=0 if self.in_kind == "u8" else 1, rows=int(self.stem_rows)))
-        elif step.kind in ("conv", "convpool"):
+        elif step.kind in ("conv", "convpool", "seppool"):
             self._emit_conv(prog, step, b)
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=self._ptr(step.res),
@@ -249,6 +278,11 @@ class XceptionEngine(EngineBase):
 
     def _emit_conv(self, prog, step: Step, b: int, split=None, cfg=None) -> None:
         H, W, OH, OW = step.geom
+        if step.kind == "seppool":
+            step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
+                            res=self._ptr(step.res), ldx=self.shapes[step.src][2], ldr=self.shapes[step.res][2],
+                            split=False, cfg=step.extra["cfg"], pool=dict(ppad=step.extra["pad"]))
+            return
         if step.kind == "convpool":
             ph, pw, pc = self.shapes[step.res]
             step.layer.emit(prog, self._ptr(step.src), self._ptr(step.dst), Geometry(b, H, W, OH, OW),
@@ -259,6 +293,65 @@ class XceptionEngine(EngineBase):
                         res=self._ptr(step.res) if step.res else None, ldx=self.shapes[step.src][2],
                         ldr=self.shapes[step.res][2] if step.res else None, tmp=self._ptr("__dwtmp"),
                         split=split, cfg=cfg)
+
+    # ------------------------------------------------------------------ chained middle flow
+    def _chainable(self, st: Step, first: Step | None) -> bool:
+        lay = st.layer
+        if (st.kind != "conv" or lay.mode != MODE_DW or lay.split or st.extra.get("branch") or st.extra.get("join")
+                or st.geom[0] != st.geom[2] or st.geom[1] != st.geom[3] or lay.relu_out not in (0, 1)):
+            return False
+        if first is None:
+            return (self.chain_cfg in CHAIN_CONFIGS and config_applicable(self.chain_cfg, st.geom[1], lay.K, lay.n)
+                    and cfg_tile(self.chain_cfg)[0] >= st.geom[1] + 1)   # 3x3 halo within M tiles mi +- 1
+        f = first.layer
+        return (st.geom == first.geom and lay.K == f.K and lay.n == f.n and lay.cin_pad == f.cin_pad
+                and self.shapes[st.src][2] == self.shapes[first.src][2]
+                and (st.res is None or self.shapes[st.res][2] == lay.ldy))
+
+    def _chain_end(self, steps: list[Step], i: int) -> int:
+        if not self.chain_cfg or not self._chainable(steps[i], None):
+            return i + 1
+        j = i + 1
+        while j < len(steps) and j - i < CHAIN_MAX_LAYERS and self._chainable(steps[j], steps[i]):
+            j += 1
+        return j
+
+    def chain_layer_args(self, steps: list[Step], b: int, maps: list[dict] | None = None) -> dict:
+        """Launch arguments of one chained launch over ``steps`` (see launch.h ChainArgs)."""
+        cfg = self.chain_cfg
+        layers, g0 = [], None
+        for k, st in enumerate(steps):
+            self._remap = maps[k] if maps else {}
+            H, W, OH, OW = st.geom
+            a = st.layer.args(self._ptr(st.src), self._ptr(st.dst), Geometry(b, H, W, OH, OW),
+                              self._ptr(st.res) if st.res else None, ldx=self.shapes[st.src][2],
+                              ldr=self.shapes[st.res][2] if st.res else None, cfg=cfg)
+            if g0 is None:
+                g0 = dict(a, relu_out=0, relu_in=0)
+            else:
+                for key in ("B", "H", "W", "M", "ldx", "ldy", "K", "NF", "nstore"):
+                    assert a[key] == g0[key], (st.name, key, a[key], g0[key])
+            if a["res"] is not None:
+                assert a["ldr"] == g0["ldy"], (st.name, a["ldr"])
+            layers.append({k2: a[k2] for k2 in ("x", "wp", "dwk", "res", "y", "bias", "relu_in", "relu_out")})
+        g0["ldr"] = g0["ldy"]
+        nM, nN = _lib.lib().sepconv_chain_tiles(cfg - SEPW_BASE, g0["M"], g0["NF"])
+        # bounded waits: ~1 us per poll, so a lost dependency costs a wait ~0.3 s, not a hang
+        return dict(g=g0, layers=layers, nM=nM, nN=nN, spin_limit=1 << 18)
+
+    def _emit_chain(self, prog, steps: list[Step], maps: list[dict], b: int) -> None:
+        d = self.chain_layer_args(steps, b, maps)
+        key = (self._slot, b, tuple(st.name for st in steps), tuple(tuple(sorted(m.items())) for m in maps))
+        n = 4 + len(steps) * d["nM"]
+        sync = self._chain_sync.get(key)
+        if sync is None:
+            # one counter block per (program, chain): programs of other slots / parities may run
+            # concurrently on other streams
+            sync = self._chain_sync[key] = torch.zeros(round_up(n, 64), dtype=torch.int32, device=self.device)
+        d["sync"] = _lib.ptr(sync)
+        name = f"chain[{steps[0].name}..{steps[-1].name}]"
+        prog.add_memset(name + "/sync", d["sync"], 4 * n)
+        prog.add_chain(name, self.chain_cfg - SEPW_BASE, d)
 
     def flops_per_image(self) -> float:
         return 2 * 8.356e9

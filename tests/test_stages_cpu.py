@@ -92,7 +92,7 @@ def test_cu_masks_are_disjoint_and_cover():
     assert sum(bin(x).count("1") for x in a + b) == 256
 
 
-def _xception_steps(fuse=False):
+def _xception_engine(fuse=False, chain=0):
     from kdl.engine import xception as XE
     from kdl.models import xception as X
 
@@ -102,11 +102,43 @@ def _xception_steps(fuse=False):
             self.max_batch, self.buckets, self.steps, self.in_kind = 1, [1], [], "u8"
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
             self.branches, self.poolfuse = 0, fuse
+            self.seppool, self.seppool_cfg, self.chain_cfg, self._chain_sync = not fuse, 0, chain, {}
 
     p = X.init_params(seed=0)
     e = Fake(p)
     e._build(p)
-    return e.steps
+    return e
+
+
+def _xception_steps(fuse=False):
+    return _xception_engine(fuse).steps
+
+
+def _runs(e, steps):
+    out, i = [], 0
+    while i < len(steps):
+        j = e._chain_end(steps, i)
+        if j - i >= 2:
+            out.append((steps[i].name, steps[j - 1].name, j - i))
+        i = max(j, i + 1)
+    return out
+
+
+def test_xception_chain_groups_the_middle_flow_within_each_stage():
+    from kdl.engine import registry
+    e = _xception_engine(chain=143)
+    # whole forward: the 24 separable convs of blocks 5-12 in one launch (block13's residual
+    # conv step comes before block13_sepconv1)
+    assert _runs(e, e.steps) == [("block5_sepconv1", "block12_sepconv3", 24)]
+    # stage-pipelined: the chain never crosses the stage cut
+    sp = _analyse(e.steps, registry.get("xception").stage_cut, scratch=["__dwtmp"])
+    got = [_runs(e, e.steps[lo:hi]) for lo, hi in sp.ranges]
+    assert got == [[("block5_sepconv1", "block7_sepconv1", 7)], [("block7_sepconv2", "block12_sepconv3", 17)]]
+    # off, or a tile whose halo does not stay within neighbouring M tiles: no chains
+    assert _runs(_xception_engine(chain=0), e.steps) == []
+    # a split (dw3x3 + GEMM) layer is not chained: it ends one run and starts none
+    e.steps[e.steps.index(next(s for s in e.steps if s.name == "block9_sepconv2"))].layer.split = True
+    assert [r[2] for r in _runs(e, e.steps)] == [13, 10]
 
 
 def test_xception_default_cut_boundaries():
