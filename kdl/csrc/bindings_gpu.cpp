@@ -181,7 +181,7 @@ ResizeArgs resize_args(const py::dict& d) {
   ResizeArgs a{};
   a.src = P<const uint8_t>(d, "src"); a.dst = P<uint8_t>(d, "dst");
   a.ytab = P<const int>(d, "ytab"); a.xtab = P<const int>(d, "xtab");
-  a.SH = I(d, "SH"); a.SW = I(d, "SW"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
+  a.SH = I(d, "SH"); a.SW = I(d, "SW"); a.OH = I(d, "OH"); a.OW = I(d, "OW"); a.n = I(d, "n", 1);
   return a;
 }
 

@@ -312,6 +312,7 @@ struct ResizeArgs {
   const int* ytab;        // [OH] source rows
   const int* xtab;        // [OW] source cols
   int SH, SW, OH, OW;
+  int n;                  // images of one source size, packed [n][SH][SW][3] -> [n][OH][OW][3] (0 = 1)
 };
 hipError_t resize_nearest_u8(const ResizeArgs& a, hipStream_t s);
 

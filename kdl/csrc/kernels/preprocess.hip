@@ -13,20 +13,24 @@ namespace kdl {
 
 __global__ __launch_bounds__(256) void resize_nearest_kernel(ResizeArgs a) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const long total = (long)a.OH * a.OW;
-  if (i >= total) return;
+  const long plane = (long)a.OH * a.OW;
+  const int img = blockIdx.y;
+  if (i >= plane) return;
   const int oy = (int)(i / a.OW), ox = (int)(i % a.OW);
+  const uint8_t* src = a.src + (long)img * a.SH * a.SW * 3;
   const long sp = ((long)a.ytab[oy] * a.SW + a.xtab[ox]) * 3;
-  const long dp = i * 3;
-  a.dst[dp] = a.src[sp];
-  a.dst[dp + 1] = a.src[sp + 1];
-  a.dst[dp + 2] = a.src[sp + 2];
+  uint8_t* dst = a.dst + (img * plane + i) * 3;
+  dst[0] = src[sp];
+  dst[1] = src[sp + 1];
+  dst[2] = src[sp + 2];
 }
 
 hipError_t resize_nearest_u8(const ResizeArgs& a, hipStream_t s) {
-  const long total = (long)a.OH * a.OW;
-  if (total <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(resize_nearest_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  const long plane = (long)a.OH * a.OW;
+  const int n = a.n > 0 ? a.n : 1;
+  if (plane <= 0 || a.SH <= 0 || a.SW <= 0 || n > 65535 || !a.src || !a.dst || !a.ytab || !a.xtab)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(resize_nearest_kernel, dim3((unsigned)((plane + 255) / 256), n), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -9,7 +9,8 @@ the reference lacks (§8.1): JSON errors (400 bad body, 502 fetch/backend errors
 mode that ships uint8 pixels to the ``serving_uint8`` signature (4x fewer bytes).
 
 Env: TF_SERVING_HOST, MODEL_NAME, SIGNATURE, INPUT_KEY, OUTPUT_KEY, LABELS,
-GATEWAY_MODE=compat|uint8, PREDICT_TIMEOUT, GATEWAY_CHANNELS (gRPC connections to open:
+GATEWAY_MODE=compat|uint8|raw (raw: decoded pixels at their own size to ``serving_image``,
+resized on the model server's GPU -- no resize here), PREDICT_TIMEOUT, GATEWAY_CHANNELS (gRPC connections to open:
 each gets its own subchannel, so a node running one model-server process per GPU on a
 shared SO_REUSEPORT port -- ``--procs`` -- sees the gateway's requests spread over all
 of them instead of pinned to whichever process accepted a single connection).
@@ -36,7 +37,10 @@ class GatewayConfig:
         self.server = env.get("TF_SERVING_HOST", "localhost:8500")
         self.model_name = env.get("MODEL_NAME", "clothing-model")
         self.mode = env.get("GATEWAY_MODE", "compat")
-        self.signature = env.get("SIGNATURE", "serving_default" if self.mode == "compat" else "serving_uint8")
+        if self.mode not in ("compat", "uint8", "raw"):
+            raise ValueError(f"GATEWAY_MODE must be compat, uint8 or raw, got {self.mode!r}")
+        self.signature = env.get("SIGNATURE", {"compat": "serving_default", "uint8": "serving_uint8",
+                                               "raw": "serving_image"}[self.mode])
         self.input_key = env.get("INPUT_KEY", "input_8" if self.mode == "compat" else "images")
         self.output_key = env.get("OUTPUT_KEY", "dense_7")
         labels = env.get("LABELS", "")
@@ -66,6 +70,8 @@ def create_app(cfg: GatewayConfig | None = None, channel: grpc.Channel | None = 
     def tensor_from_image(img):
         if cfg.mode == "uint8":
             return pp.to_uint8(img)[None]
+        if cfg.mode == "raw":
+            return np.asarray(img, dtype=np.uint8)[None]
         return pp.image_to_tensor(img)
 
     def run(X: np.ndarray):
@@ -111,11 +117,14 @@ def create_app(cfg: GatewayConfig | None = None, channel: grpc.Channel | None = 
         if not isinstance(urls, list) or not urls or not all(isinstance(u, str) for u in urls):
             return fail(400, 'request body must be JSON {"urls": ["<image url>", ...]}')
         try:
-            X = np.concatenate([tensor_from_image(load(u)) for u in urls])
+            Xs = [tensor_from_image(load(u)) for u in urls]
         except LookupError as e:
             return fail(502, str(e))
         try:
-            pb_result = run(X)
+            if cfg.mode == "raw" and len({x.shape for x in Xs}) > 1:
+                # raw pixels of different sizes cannot share one dense tensor: one request each
+                return jsonify([process_response(run(x), cfg.labels, cfg.output_key) for x in Xs])
+            pb_result = run(np.concatenate(Xs))
         except grpc.RpcError as e:
             return grpc_fail(e)
         return jsonify(process_batch_response(pb_result, cfg.labels, cfg.output_key))

@@ -16,7 +16,8 @@ Backends:
   * ``cpu``: the family's fp32 torch oracle ("config #1: plumbing, no GPU").
 
 Families: ``xception`` (the reference's clothing model; SavedModel ingest,
-``serving_default`` = f32 ``input_8`` like TF-Serving, plus ``serving_uint8``),
+``serving_default`` = f32 ``input_8`` like TF-Serving, plus ``serving_uint8`` and
+``serving_image`` = uint8 images of any size, resized on the GPU: resize.py),
 and ``resnet50`` / ``vit_b16`` / ``efficientnet_b7`` (BASELINE.json configs;
 torchvision-layout safetensors or synthetic weights, uint8 ``images`` input).
 """
@@ -38,6 +39,7 @@ from ..ops import _lib
 from . import protos as P
 from .config import ServerConfig
 from .metrics import BATCH_BUCKETS, METRICS
+from .resize import IMAGE_SIGNATURE, ImageRunner
 
 log = logging.getLogger("kdl.serving")
 
@@ -86,6 +88,8 @@ def _family_source(family: str, params: dict | None, seed: int, origin: str) -> 
     S, n = info.input_size, info.classes
     sigs = {name: SignatureInfo(name, NATIVE_INPUT_KEY, P.DT_UINT8, "logits", input_shape=(-1, S, S, 3),
                                 output_shape=(-1, n)) for name in ("serving_default", NATIVE_SIGNATURE)}
+    sigs[IMAGE_SIGNATURE] = SignatureInfo(IMAGE_SIGNATURE, NATIVE_INPUT_KEY, P.DT_UINT8, "logits",
+                                          input_shape=(-1, -1, -1, 3), output_shape=(-1, n))
     return ModelSource(params=params, head=None, signatures=sigs, origin=origin, family=family,
                        input_size=S, classes=n)
 
@@ -133,6 +137,9 @@ def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
     out_key = sigs["serving_default"].output_key
     sigs.setdefault(NATIVE_SIGNATURE, SignatureInfo(NATIVE_SIGNATURE, NATIVE_INPUT_KEY, P.DT_UINT8, out_key,
                                                     output_shape=(-1, head.classes)))
+    # any-size uint8 images, resized on the GPU (serving/resize.py)
+    sigs.setdefault(IMAGE_SIGNATURE, SignatureInfo(IMAGE_SIGNATURE, NATIVE_INPUT_KEY, P.DT_UINT8, out_key,
+                                                   input_shape=(-1, -1, -1, 3), output_shape=(-1, head.classes)))
     return ModelSource(params=params, head=head, signatures=sigs, origin=origin, classes=head.classes)
 
 
@@ -636,7 +643,7 @@ class Servable:
         self.signatures = source.signatures
         self.runners: dict[str, SignatureRunner] = {}
         self._devices, self._cfg = devices, cfg
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()     # serving_image builds its serving_uint8 runner inside
         # serving_default is warmed eagerly (readiness = its graphs are captured), plus any
         # --warm_signatures (TF-Serving's warmup analogue: engines built before traffic arrives)
         self.runner("serving_default")
@@ -651,8 +658,11 @@ class Servable:
                 if sig_name not in self.signatures:
                     raise ServingError("INVALID_ARGUMENT", f"Serving signature name: \"{sig_name}\" not found "
                                        "in signature def")
-                r = self.runners[sig_name] = SignatureRunner(self.signatures[sig_name], self.source,
-                                                             self._cfg, self._devices)
+                if sig_name == IMAGE_SIGNATURE and NATIVE_SIGNATURE in self.signatures:
+                    r = ImageRunner(self.signatures[sig_name], self.runner(NATIVE_SIGNATURE), self._devices)
+                else:
+                    r = SignatureRunner(self.signatures[sig_name], self.source, self._cfg, self._devices)
+                self.runners[sig_name] = r
             return r
 
     def healthy(self) -> bool:

@@ -44,6 +44,8 @@ def _payload(raw: bytes, td: dict, sig) -> tuple[object, int]:
     """Return (buffer of n images in the signature's dtype, n) from a parsed input."""
     dims = list(td["dims"])
     IMG = sig.input_shape[1]
+    if IMG == -1:           # serving_image: uint8 [n, H, W, 3] of any size
+        return _image_payload(raw, td, sig, dims)
     if td["dtype"] != sig.input_dtype:
         raise ServingError("INVALID_ARGUMENT",
                            f"Expects arg[0] to be {P.DTYPE_NAMES.get(sig.input_dtype)} but "
@@ -76,6 +78,29 @@ def _payload(raw: bytes, td: dict, sig) -> tuple[object, int]:
     arr = np.ascontiguousarray(arr.reshape(n, IMG, IMG, 3),
                                dtype=np.uint8 if sig.input_dtype == P.DT_UINT8 else np.float32)
     return arr, n
+
+
+def _image_payload(raw: bytes, td: dict, sig, dims: list) -> tuple[np.ndarray, int]:
+    if td["dtype"] != P.DT_UINT8:
+        raise ServingError("INVALID_ARGUMENT", f"Expects arg[0] to be uint8 but "
+                           f"{P.DTYPE_NAMES.get(td['dtype'], td['dtype'])} is provided")
+    if len(dims) != 4 or dims[3] != 3 or min(dims[:3]) < 1:
+        raise ServingError("INVALID_ARGUMENT", f"input '{sig.input_key}' must have shape [-1,-1,-1,3], got {dims}")
+    n, H, W = dims[:3]
+    need = n * H * W * 3
+    if td["has_content"]:
+        if td["size"] != need:
+            raise ServingError("INVALID_ARGUMENT", f"tensor content has {td['size']} bytes, expected {need}")
+        arr = np.frombuffer(raw, dtype=np.uint8, count=need, offset=td["offset"])
+    else:
+        try:
+            arr = P.tensor_proto_to_np(P.PredictRequest.FromString(raw).inputs[td["key"]]).astype(np.uint8)
+        except (ValueError, KeyError, TypeError) as e:
+            raise ServingError("INVALID_ARGUMENT", f"cannot decode input '{sig.input_key}': {e}") from e
+        if arr.size != need:
+            raise ServingError("INVALID_ARGUMENT", f"input '{sig.input_key}' has {arr.size} values, but its "
+                               f"shape {dims} needs {need}")
+    return arr.reshape(n, H, W, 3), n
 
 
 class Servicer:

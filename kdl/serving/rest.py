@@ -104,7 +104,10 @@ def make_handler(manager: ModelManager):
                 else:
                     raise ServingError("INVALID_ARGUMENT", "request must contain 'instances' or 'inputs'")
                 S = sig.input_shape[1]
-                if x.ndim != 4 or x.shape[1:] != (S, S, 3):
+                if S == -1:          # serving_image: any size
+                    if x.ndim != 4 or x.shape[3] != 3 or min(x.shape) < 1:
+                        raise ServingError("INVALID_ARGUMENT", f"expected images [-1,-1,-1,3], got {list(x.shape)}")
+                elif x.ndim != 4 or x.shape[1:] != (S, S, 3):
                     raise ServingError("INVALID_ARGUMENT", f"expected images [-1,{S},{S},3], got {list(x.shape)}")
                 x = np.ascontiguousarray(x)
                 dl = self.headers.get("X-Deadline-Ms")

@@ -195,6 +195,42 @@ def test_gateway_uint8_mode_matches_compat(server, image_server):
     assert all(abs(ga[k] - gb[k]) < 1e-3 for k in ga)
 
 
+def test_gateway_raw_mode_resizes_on_the_server(server, image_server):
+    """GATEWAY_MODE=raw ships the decoded pixels at their own size to serving_image; the server's
+    resize (PIL NEAREST tables) makes it exactly the uint8 mode's prediction."""
+    base = {"TF_SERVING_HOST": f"127.0.0.1:{server.grpc_port}"}
+    a = create_app(GatewayConfig({**base, "GATEWAY_MODE": "uint8"})).test_client().post(
+        "/predict", json={"url": f"{image_server}/pants.png"})
+    b = create_app(GatewayConfig({**base, "GATEWAY_MODE": "raw"})).test_client().post(
+        "/predict", json={"url": f"{image_server}/pants.png"})
+    assert a.status_code == b.status_code == 200, b.data
+    assert a.get_json() == b.get_json()
+    with pytest.raises(ValueError):
+        GatewayConfig({**base, "GATEWAY_MODE": "bogus"})
+
+
+@pytest.mark.parametrize("shape", [(1, 534, 400), (2, 1, 1), (1, 2200, 300), (1, 299, 299)])
+def test_serving_image_any_size_equals_pil_resize(channel, shape):
+    n, H, W = shape
+    rng = np.random.default_rng(H * 7 + W)
+    raw = rng.integers(0, 256, (n, H, W, 3), dtype=np.uint8)
+    from PIL import Image
+    pil = np.stack([np.asarray(Image.fromarray(im).resize((299, 299), Image.NEAREST)) for im in raw])
+    stub = PredictionStub(channel)
+    r1 = stub.Predict(make_request(raw, signature="serving_image", input_key="images"), timeout=30.0)
+    r2 = stub.Predict(make_request(pil, signature="serving_uint8", input_key="images"), timeout=30.0)
+    a = np.asarray(r1.outputs["dense_7"].float_val)
+    assert a.size == n * 10 and np.array_equal(a, np.asarray(r2.outputs["dense_7"].float_val))
+
+
+def test_serving_image_rejects_bad_shapes(channel):
+    stub = PredictionStub(channel)
+    for bad in (np.zeros((1, 5, 5, 4), np.uint8), np.zeros((1, 5, 5, 3), np.float32)):
+        with pytest.raises(grpc.RpcError) as e:
+            stub.Predict(make_request(bad, signature="serving_image", input_key="images"), timeout=5)
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+
+
 def test_deadline_exceeded(channel):
     stub = PredictionStub(channel)
     x = np.zeros((4, 299, 299, 3), np.float32)

@@ -45,6 +45,23 @@ def test_gpu_predict_matches_oracle(gpu_server):
     assert np.abs(got8 - ref).max() < 0.05 * scale
 
 
+def test_gpu_serving_image_resizes_on_device_exactly(gpu_server):
+    """serving_image: any-size uint8 images, resized by the HIP kernel on the server's GPU,
+    give bit-for-bit the logits of serving_uint8 fed with PIL-NEAREST-resized images."""
+    from PIL import Image
+    from kdl.serving.resize import Resizer
+    stub = PredictionStub(grpc.insecure_channel(f"127.0.0.1:{gpu_server.grpc_port}"))
+    for n, H, W in [(1, 534, 400), (2, 1, 1), (1, 2200, 2200)]:
+        raw = np.random.default_rng(H).integers(0, 256, (n, H, W, 3), dtype=np.uint8)
+        pil = np.stack([np.asarray(Image.fromarray(im).resize((299, 299), Image.NEAREST)) for im in raw])
+        r1 = stub.Predict(make_request(raw, signature="serving_image", input_key="images"), timeout=60)
+        r2 = stub.Predict(make_request(pil, signature="serving_uint8", input_key="images"), timeout=60)
+        a = np.asarray(r1.outputs["dense_7"].float_val, np.float32)
+        assert a.size == 10 * n and np.array_equal(a, np.asarray(r2.outputs["dense_7"].float_val, np.float32))
+    s = gpu_server.manager.get("clothing-model", None, None)
+    assert s.runner("serving_image").resizer.device is not None, "resize ran on the CPU"
+
+
 def test_rccl_world1_dp_runner():
     import torch.distributed as dist
 

@@ -2,6 +2,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 tools/gpu_session.sh \
   chain 240 python -u -m pytest tests/test_kernels_gpu.py -v -x --timeout 110 --timeout-method thread -k "chained" -- \
+  resize 200 python -u -m pytest tests/test_resize.py tests/test_serving_gpu.py -v --timeout 110 --timeout-method thread -k "resize" -- \
   ktests 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_serving_gpu.py -v --timeout 200 --timeout-method thread -k "sepconv_pool or seppool or native or separable" -- \
   gate 200 python -u -m pytest tests/test_bench_configs_gpu.py -v -rP --timeout 150 --timeout-method thread -k xception -- \
   b_on1 100 python bench.py --steps 200 --warmup 20 -- \
