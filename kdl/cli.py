@@ -1,7 +1,8 @@
 """``python -m kdl.cli <command>``: TF-free model tooling.
 
   show <saved_model_dir>                     saved_model_cli-style signature dump (guide.md:202)
-  convert-savedmodel <saved_model_dir> <out> SavedModel -> kdl_params.safetensors + kdl_model.json
+  convert-savedmodel <saved_model_dir> <out> SavedModel -> kdl_params.safetensors (the Keras fp32
+                                             variables, unfolded) + kdl_model.json (head, signatures)
   make-synthetic <repo>/<version> [--seed] [--model xception|resnet50|vit_b16|efficientnet_b7]
                                              random-init weights of the exact architecture (Xception:
                                              a SavedModel; other families: torchvision-layout safetensors)

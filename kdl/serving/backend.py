@@ -357,6 +357,10 @@ class GPUExecutor(_Executor):
             cut = info.stage_cut
         if cut and cut != "none" and self.lanes is None and hasattr(self.engine, "alias_buffer"):
             from ..engine.stages import StagePipe
+            # its own engine ON PURPOSE: a top-bucket batch in the pipe and a small-bucket batch
+            # in self.engine's graphs can be in flight together (depth >= 2, different streams),
+            # so they must not share activation buffers; the duplicate costs ~50 MB of packed
+            # weights + the activations of one batch, next to 288 GB of HBM
             self.pipe = StagePipe(make(bs[-1]), cut)
             if tp.exists():
                 self.pipe.load_tuning(tp)

@@ -74,6 +74,8 @@ class ServerConfig:
     procs: int = 1
     gpu_index: int = -1
     warm_signatures: list[str] = field(default_factory=list)   # built at load, besides serving_default
+    log_format: str = "text"      # text | json (one JSON object per line, for log shippers)
+    stats_log_interval_s: float = 0.0   # > 0: a "stats" log record (metrics snapshot) this often
 
     def executors_for(self, n_devices: int) -> int:
         """Executors per device: --executors_per_gpu when given, else TF-Serving's
@@ -132,6 +134,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--warm_signatures", default="",
                     help="comma list of signatures whose engines / graphs are built at model load (like "
                          "TF-Serving warmup requests); serving_default always is")
+    ap.add_argument("--log_format", choices=["text", "json"], default=None,
+                    help="json: one JSON object per log line (env KDL_LOG_FORMAT)")
+    ap.add_argument("--stats_log_interval_s", type=float, default=None,
+                    help="log a metrics snapshot (requests, latency quantiles, batch sizes, queue depth, "
+                         "per-GPU busy ratio) every N seconds; 0 = off (env KDL_STATS_LOG_INTERVAL_S)")
     return ap
 
 
@@ -169,4 +176,7 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         lanes=a.lanes if a.lanes is not None else int(env.get("KDL_LANES", "1")),
                         exec_depth=a.exec_depth if a.exec_depth is not None else int(env.get("KDL_EXEC_DEPTH", "2")),
                         procs=max(1, a.procs), gpu_index=a.gpu_index,
-                        warm_signatures=[s for s in a.warm_signatures.split(",") if s])
+                        warm_signatures=[s for s in a.warm_signatures.split(",") if s],
+                        log_format=a.log_format or env.get("KDL_LOG_FORMAT", "text"),
+                        stats_log_interval_s=(a.stats_log_interval_s if a.stats_log_interval_s is not None
+                                              else float(env.get("KDL_STATS_LOG_INTERVAL_S", "0"))))

@@ -103,5 +103,26 @@ class Metrics:
                 pass
         return "\n".join(out) + "\n"
 
+    def snapshot(self) -> dict:
+        """Counters, histogram summaries (count, mean, p50, p99) and gauges as one JSON-able
+        dict (the periodic "stats" log record). Reading a rate gauge here starts its next
+        window, like a scrape does."""
+        def key(name, labels):
+            return name + ("{" + ",".join(f"{k}={v}" for k, v in labels) + "}" if labels else "")
+        out: dict = {"counters": {}, "histograms": {}, "gauges": {}}
+        with self._lock:
+            for (name, labels), v in sorted(self.counters.items()):
+                out["counters"][key(name, labels)] = v
+            for (name, labels), h in sorted(self.hists.items()):
+                out["histograms"][key(name, labels)] = {
+                    "count": h.n, "mean": h.sum / h.n if h.n else 0.0, "p50": h.quantile(0.5), "p99": h.quantile(0.99)}
+            gauges = list(self.gauges.items())
+        for (name, labels), fn in sorted(gauges, key=lambda kv: kv[0]):
+            try:
+                out["gauges"][key(name, labels)] = float(fn())
+            except Exception:  # noqa: BLE001 - a broken gauge must not break the record
+                pass
+        return out
+
 
 METRICS = Metrics()

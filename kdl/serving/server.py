@@ -16,6 +16,7 @@ import time
 
 from .config import ServerConfig, config_from_args
 from .grpc_server import build_grpc_server
+from .logs import StatsLogger, setup_logging
 from .model_repo import ModelManager
 from .rest import start_rest_server
 
@@ -104,13 +105,14 @@ def launch_procs(argv: list[str], cfg: ServerConfig) -> int:
 
 
 def main(argv=None) -> int:
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s",
-                        stream=sys.stdout)
     argv = list(sys.argv[1:] if argv is None else argv)
     cfg = config_from_args(argv)
+    setup_logging(cfg.log_format)
     if cfg.procs > 1:
         return launch_procs(argv, cfg)
     srv = ModelServer(cfg).start(block_until_loaded=False)
+    if cfg.stats_log_interval_s > 0:
+        StatsLogger(cfg.stats_log_interval_s).start()
     done = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *_: done.set())

@@ -63,3 +63,45 @@ def test_num_batch_threads_sets_concurrent_executors(tmp_path):
     cfg = config_from_args([f"--batching_parameters_file={f}", "--executors_per_gpu=3"], env={})
     assert cfg.executors_for(8) == 3
     assert config_from_args([], env={}).executors_for(8) == 1
+
+
+def test_json_logs_and_stats_snapshot():
+    import io
+    import json
+    import logging
+
+    from kdl.serving.config import config_from_args
+    from kdl.serving.logs import StatsLogger, setup_logging
+    from kdl.serving.metrics import Metrics
+
+    cfg = config_from_args(["--log_format=json", "--stats_log_interval_s=0.05"], env={})
+    assert cfg.log_format == "json" and cfg.stats_log_interval_s == 0.05
+    assert config_from_args([], env={"KDL_LOG_FORMAT": "json"}).log_format == "json"
+    assert config_from_args([], env={}).log_format == "text"
+    buf = io.StringIO()
+    old = logging.getLogger().handlers[:]
+    try:
+        setup_logging("json", buf)
+        logging.getLogger("kdl.serving").info("loaded %s", "m", extra={"version": 3})
+        rec = json.loads(buf.getvalue().splitlines()[-1])
+        assert rec["msg"] == "loaded m" and rec["version"] == 3 and rec["level"] == "INFO" and rec["pid"] > 0
+        m = Metrics()
+        m.inc("kdl_requests_total", code="OK")
+        for v in (1.0, 2.0, 3.0):
+            m.observe("kdl_request_latency_ms", v)
+        m.gauge("kdl_gpu_busy_ratio", lambda: 0.5, executor="gpu0")
+        snap = m.snapshot()
+        assert snap["counters"]["kdl_requests_total{code=OK}"] == 1
+        h = snap["histograms"]["kdl_request_latency_ms"]
+        assert h["count"] == 3 and h["p50"] == 2.0 and h["mean"] == 2.0
+        assert snap["gauges"]["kdl_gpu_busy_ratio{executor=gpu0}"] == 0.5
+        sl = StatsLogger(0.02)
+        sl.start()
+        import time
+        time.sleep(0.15)
+        sl.stop.set()
+        sl.join(2)
+        stats = [json.loads(l) for l in buf.getvalue().splitlines() if '"event": "stats"' in l]
+        assert stats and "counters" in stats[0] and "gauges" in stats[0]
+    finally:
+        logging.getLogger().handlers[:] = old
