@@ -7,12 +7,14 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
     conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
     conv_gemm MODE_PW    residual 1x1/2 convs + BN (KDL_POOLFUSE=1: with the block's
                          3x3/2 max-pool of the main branch added in the epilogue, "convpool")
-    seppool              an entry block's last SeparableConv2D + its 3x3/2 max-pool + the
-                         residual add in ONE kernel (sepconv_2dwp_kernel, "seppool" steps;
-                         KDL_SEP_POOL=0 restores conv + pool_add); where no pooled config
-                         fits (wide K x N weights), pool_add:
+    seppool              KDL_SEP_POOL=1: an entry block's last SeparableConv2D + its 3x3/2
+                         max-pool + the residual add in ONE kernel (sepconv_2dwp_kernel,
+                         "seppool" steps; measured slower, off by default); otherwise:
     pool_add             TF-'same' 3x3/2 max-pool + residual add
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
+
+    chain                KDL_CHAIN=<ws cfg>: the middle flow's separable convs as ONE ticketed
+                         launch per program (sepconv_chain_kernel; off by default, see __init__)
 
 = 41 launches per forward (vs ~168 unfused TF ops), captured into
 one hipGraph per batch bucket. All buffers are allocated once for the largest
@@ -59,14 +61,22 @@ class XceptionEngine(EngineBase):
         # dependent 16-B pool reads per output chunk are latency-bound inside the GEMM's store
         # loop, so the fused launch (80.8 us at block2) costs what conv + pool_add did (82.6)
         self.poolfuse = os.environ.get("KDL_POOLFUSE", "0") == "1" and not self.branches
-        # KDL_SEP_POOL (default on): the block's last separable conv writes maxpool + residual
-        # directly (sepconv_2dwp_kernel); bit-identical to conv + pool_add
-        self.seppool = os.environ.get("KDL_SEP_POOL", "1") != "0" and not self.poolfuse
+        # KDL_SEP_POOL=1: the block's last separable conv writes maxpool + residual directly
+        # (sepconv_2dwp_kernel); bit-identical to conv + pool_add. Off by default: block2's
+        # pooled launch took 275 us vs ~170 for sepconv + pool_add (it recomputes the pool
+        # windows' overlap rows), 20.5-21.1k vs 22.6k img/s in the pipelined bench
+        # (profiles/seppool_chain_ab_r3.txt)
+        self.seppool = os.environ.get("KDL_SEP_POOL", "0") == "1" and not self.poolfuse
         self.seppool_cfg = int(os.environ.get("KDL_SEP_POOL_CFG", "0"))
         # KDL_CHAIN=<cfg> (0 = off): each run of same-geometry separable convs inside one
-        # program (the middle flow: blocks 5-12 + block13_sepconv1, split only at a stage cut)
-        # becomes ONE chained launch (sepconv_chain_kernel, launch.h ChainArgs) with that ws tile
+        # program (the middle flow: blocks 5-12, split only at a stage cut) becomes ONE chained
+        # launch (sepconv_chain_kernel, launch.h ChainArgs) with that ws tile. Alone it is 7 %
+        # faster per layer (29.6 vs ~32 us at batch 32: no launch, fill or drain per layer), but
+        # in the stage-pipelined bench the other stream's kernels already fill those gaps while
+        # the chain's dependency-waiting workgroups hold CUs: 20.5k vs 21.0k img/s
+        # (profiles/seppool_chain_ab_r3.txt). Off by default.
         self.chain_cfg = int(os.environ.get("KDL_CHAIN", "0"))
+        self.chain_min = int(os.environ.get("KDL_CHAIN_MIN", "2"))      # shortest run worth chaining
         self._chain_sync: dict[tuple, torch.Tensor] = {}
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
@@ -314,7 +324,7 @@ class XceptionEngine(EngineBase):
         j = i + 1
         while j < len(steps) and j - i < CHAIN_MAX_LAYERS and self._chainable(steps[j], steps[i]):
             j += 1
-        return j
+        return j if j - i >= self.chain_min else i + 1
 
     def chain_layer_args(self, steps: list[Step], b: int, maps: list[dict] | None = None) -> dict:
         """Launch arguments of one chained launch over ``steps`` (see launch.h ChainArgs)."""

@@ -103,6 +103,7 @@ def _xception_engine(fuse=False, chain=0):
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
             self.branches, self.poolfuse = 0, fuse
             self.seppool, self.seppool_cfg, self.chain_cfg, self._chain_sync = not fuse, 0, chain, {}
+            self.chain_min = 2
 
     p = X.init_params(seed=0)
     e = Fake(p)
