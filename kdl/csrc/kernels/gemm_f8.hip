@@ -170,7 +170,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
   X(4, 3, 3, 2, 4, 2)     \
   X(5, 6, 3, 2, 4, 2)     \
   X(6, 3, 6, 2, 4, 2)     \
-  X(7, 4, 4, 2, 4, 2)
+  X(7, 4, 4, 2, 4, 2)     \
+  X(8, 5, 2, 2, 4, 2)     \
+  X(9, 5, 3, 2, 4, 2)     \
+  X(10, 5, 4, 2, 4, 2)
+// 8-10: 160-row tiles, whole waves of 256 CUs at the ViT-B/16 token count (gemm_pipe.hip 45-47)
 
 int gemm_f8_config(int cfg, int* bm, int* bn, int* threads) {
   switch (cfg) {

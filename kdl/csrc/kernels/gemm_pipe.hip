@@ -241,7 +241,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   X(23, 3, 6, 2, 4, 5, 1)   \
   X(24, 3, 3, 2, 4, 6, 1)   \
   X(25, 4, 2, 2, 4, 6, 1)   \
-  X(26, 6, 3, 2, 4, 3, 2)
+  X(26, 6, 3, 2, 4, 3, 2)    \
+  X(45, 5, 2, 2, 4, 3, 1)   \
+  X(46, 5, 3, 2, 4, 3, 1)   \
+  X(47, 5, 4, 2, 4, 3, 1)
+// 45-47: 160-row tiles (ids after the ablations). At the ViT-B/16 shapes (M = 32 x 197 =
+// 6304 rows) they fill 256 CUs in whole waves: out_proj / mlp.3 (N 768) 160x128 -> 240
+// tiles; QKV (N 2304) 160x192 -> 480; mlp.0 (N 3072) 160x256 -> 480 (vs 192x192: 396 / 528)
 
 // timing ablations of id 9 (ABL bits above), ids 27..44
 #define KDL_PIPE_ABL(X) \
@@ -302,7 +308,7 @@ hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& args, hipStream_t s)
   static const int env_krot = [] { const char* e = getenv("KDL_PIPE_KROT"); return e ? atoi(e) : -1; }();
   ConvGemmArgs a = args;
   if (env_krot >= 0) a.krot = env_krot;
-  if (cfg >= 27) return mode == 0 && a.dt == 0 ? launch_pipe_ablation(cfg, a, s) : hipErrorInvalidValue;
+  if (cfg >= 27 && cfg <= 44) return mode == 0 && a.dt == 0 ? launch_pipe_ablation(cfg, a, s) : hipErrorInvalidValue;
   if (mode == 0) return a.dt ? launch_pipe_mode<0, 1>(cfg, a, s) : launch_pipe_mode<0, 0>(cfg, a, s);
   if (mode == 1) return a.dt ? launch_pipe_mode<1, 1>(cfg, a, s) : launch_pipe_mode<1, 0>(cfg, a, s);
   return hipErrorInvalidValue;

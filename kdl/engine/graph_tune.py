@@ -68,7 +68,8 @@ def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
 
 
 def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, margin: float = 0.002,
-               log=print) -> dict:
+               log=print, only: set | None = None) -> dict:
+    """``only``: challenge the incumbents with these tile configs only (e.g. newly added ids)."""
     table = dict(eng.tuning())
     eng.apply_tuning(table)
     base = statistics.median(graph_time(eng, b, reps) for _ in range(3))
@@ -80,8 +81,9 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
         for i, step in enumerate(steps):
             name = step.name
             cur = table[name]
-            log(f"  [{i + 1}/{len(steps)}] {name} ({len(_variants_of(eng, step))} variants) at {base * 1e3:.1f} us")
-            for split, cfg in _variants_of(eng, step):
+            variants = [v for v in _variants_of(eng, step) if only is None or v[1] in only]
+            log(f"  [{i + 1}/{len(steps)}] {name} ({len(variants)} variants) at {base * 1e3:.1f} us")
+            for split, cfg in variants:
                 cand = [int(split), int(cfg)]
                 if cand == cur:
                     continue
@@ -123,6 +125,7 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--start", default=None, help="starting table (default: the committed table)")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--cfgs", default=None, help="comma list: only these configs challenge the table")
     a = ap.parse_args(argv)
     from . import registry
     from .tuning import tuning_path
@@ -151,7 +154,8 @@ def main(argv=None) -> int:
     else:
         inp.copy_(torch.rand(tuple(inp.shape), generator=g) * 2 - 1)
     t0 = time.time()
-    table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True))
+    only = {int(c) for c in a.cfgs.split(",")} if a.cfgs else None
+    table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only)
     Path(a.out).write_text(json.dumps(table, indent=1))
     print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
     return 0

@@ -38,6 +38,8 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            48: (6, 3, 2, 4), 49: (6, 3, 2, 4), 50: (6, 3, 2, 4), 51: (6, 3, 2, 4),
            52: (6, 3, 2, 4), 53: (6, 3, 2, 4), 54: (6, 3, 2, 4), 55: (6, 3, 2, 4), 56: (6, 3, 2, 4),
            57: (6, 3, 2, 4), 58: (6, 3, 2, 4), 59: (6, 3, 2, 4), 60: (6, 3, 2, 4),
+           # 160-row LDS-DMA tiles (gemm_pipe.hip ids 45-47): whole waves at the ViT token counts
+           61: (5, 2, 2, 4), 62: (5, 3, 2, 4), 63: (5, 4, 2, 4),
            # warp-specialized fused separable conv (sepconv_ws.hip, KDL_SEPW_CONFIGS): (FM, FN, 1, 4);
            # 127 = s_memtime stamping build of 121 (tools/stamps.py, never a candidate)
            120: (6, 6, 1, 4), 121: (6, 6, 1, 4), 122: (6, 6, 1, 4), 123: (6, 6, 1, 4), 124: (6, 3, 1, 4),
@@ -78,9 +80,9 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
            135: 15, 136: 11, 137: 15, 140: 8, 141: 8, 142: 8,
            143: 9, 144: 11, 145: 16, 146: 8}
-# never autotune candidates: gemm_pipe timing ablations (KDL_PIPE_ABL), the ws stamping build
 # ws configs with a chained (multi-layer, one launch) variant: sepconv_ws.hip KDL_CHAIN_CONFIGS
 CHAIN_CONFIGS = (143, 144, 146)
+# never autotune candidates: gemm_pipe timing ablations (KDL_PIPE_ABL), the ws stamping build
 ABLATION_IDS = frozenset(list(range(43, 61)) + [127] + list(S2DWP))
 
 
