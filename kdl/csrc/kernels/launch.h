@@ -67,7 +67,8 @@ int sepconv_ws_fits(int cfg, int W);
 // in layer-major order and a tile of layer l starts once the three M tiles of layer l-1 whose
 // rows its 3x3 halo reads are published (write-through stores + per-(layer, M tile) counters,
 // agent-scope acquire). Deadlock-free at any residency: a ticket's dependencies were taken
-// earlier, by workgroups that are running. `sync` must be zeroed before every launch.
+// earlier, by workgroups that are running. sepconv_chain zeroes `sync` (4 + nlayers * nM ints)
+// with a kernel of its own ahead of every chain launch.
 struct ChainArgs {
   static constexpr int MAXL = 32;
   ConvGemmArgs g;               // shared geometry / flags (its pointers unused)

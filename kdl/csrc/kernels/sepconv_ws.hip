@@ -404,6 +404,10 @@ __global__ __launch_bounds__(512) void sepconv_chain_kernel(ChainArgs c) {
   if (tid == 0) *s_item = __hip_atomic_fetch_add(c.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int item = __builtin_amdgcn_readfirstlane(*s_item);
+  if (item >= tiles * c.nlayers) {              // a counter not zeroed before the launch: flag it,
+    if (tid == 0) __hip_atomic_store(c.sync + 1, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;                                     // never index past the layer tables (uniform exit)
+  }
   const int layer = item / tiles, t = item - layer * tiles;
   const int mi = t / c.nN, ni = t - mi * c.nN;
   if (tid == 0) {
@@ -543,6 +547,13 @@ int sepconv_chain_tiles(int cfg, int M, int NF, int* nM, int* nN) {
   }
 }
 
+// Zeroes the chain's ticket / error / counter block ahead of every chain launch (a kernel node
+// of its own in the captured graph; a captured hipMemsetAsync node re-zeroed it on the first
+// replay only: tools/chain_diag.py measured 531,776 tickets on the second).
+__global__ __launch_bounds__(256) void chain_reset_kernel(int* p, int n) {
+  for (int i = threadIdx.x; i < n; i += 256) p[i] = 0;
+}
+
 hipError_t sepconv_chain(int cfg, const ChainArgs& c, hipStream_t s) {
   const ConvGemmArgs& g = c.g;
   int nM = 0, nN = 0;
@@ -551,6 +562,8 @@ hipError_t sepconv_chain(int cfg, const ChainArgs& c, hipStream_t s) {
       g.OW != g.W || g.M <= 0 || c.spin_limit < 1 || chain_bm(cfg) < g.W + 1)   // halo within mi +- 1
     return hipErrorInvalidValue;
   const int grid = nM * nN * c.nlayers;        // one workgroup per ticket
+  hipLaunchKernelGGL(chain_reset_kernel, dim3(1), dim3(256), 0, s, c.sync, 4 + nM * c.nlayers);
+  if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   switch (cfg) {
 #define KDL_CHCASE(id, fm, fn, st, xb) \
   case id: hipLaunchKernelGGL((sepconv_chain_kernel<fm, fn, st, xb>), dim3(grid), dim3(512), 0, s, c); break;

@@ -68,8 +68,12 @@ def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
 
 
 def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, margin: float = 0.002,
-               log=print, only: set | None = None) -> dict:
-    """``only``: challenge the incumbents with these tile configs only (e.g. newly added ids)."""
+               log=print, only: set | None = None, tie: str | None = None) -> dict:
+    """``only``: challenge the incumbents with these tile configs only (e.g. newly added ids).
+    ``tie``: regex; steps whose names are equal once it is replaced by '*' move together (the
+    12 identical encoder layers of a ViT: one layer's few-us win sits inside the margin, the
+    same tile on all twelve does not)."""
+    import re
     table = dict(eng.tuning())
     eng.apply_tuning(table)
     base = statistics.median(graph_time(eng, b, reps) for _ in range(3))
@@ -78,16 +82,19 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
     for p in range(passes):
         changed = 0
         steps = _steps_of(eng)
-        for i, step in enumerate(steps):
-            name = step.name
-            cur = table[name]
+        groups: dict[str, list] = {}
+        for st in steps:
+            groups.setdefault(re.sub(tie, "*", st.name) if tie else st.name, []).append(st)
+        for i, (gname, members) in enumerate(groups.items()):
+            step, name = members[0], gname
+            cur = table[step.name]
             variants = [v for v in _variants_of(eng, step) if only is None or v[1] in only]
-            log(f"  [{i + 1}/{len(steps)}] {name} ({len(variants)} variants) at {base * 1e3:.1f} us")
+            log(f"  [{i + 1}/{len(groups)}] {name} x{len(members)} ({len(variants)} variants) at {base * 1e3:.1f} us")
             for split, cfg in variants:
                 cand = [int(split), int(cfg)]
                 if cand == cur:
                     continue
-                trial = dict(table, **{name: cand})
+                trial = dict(table, **{m.name: cand for m in members})
                 eng.apply_tuning(trial)
                 t = graph_time(eng, b, reps)
                 if t >= base * (1 - margin):
@@ -126,6 +133,7 @@ def main(argv=None) -> int:
     ap.add_argument("--start", default=None, help="starting table (default: the committed table)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--cfgs", default=None, help="comma list: only these configs challenge the table")
+    ap.add_argument("--tie", default=None, help=r"regex, e.g. 'encoder_layer_\d+': tune matching layers together")
     a = ap.parse_args(argv)
     from . import registry
     from .tuning import tuning_path
@@ -155,7 +163,8 @@ def main(argv=None) -> int:
         inp.copy_(torch.rand(tuple(inp.shape), generator=g) * 2 - 1)
     t0 = time.time()
     only = {int(c) for c in a.cfgs.split(",")} if a.cfgs else None
-    table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only)
+    table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only,
+                       tie=a.tie)
     Path(a.out).write_text(json.dumps(table, indent=1))
     print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
     return 0

@@ -358,10 +358,8 @@ class XceptionEngine(EngineBase):
             # one counter block per (program, chain): programs of other slots / parities may run
             # concurrently on other streams
             sync = self._chain_sync[key] = torch.zeros(round_up(n, 64), dtype=torch.int32, device=self.device)
-        d["sync"] = _lib.ptr(sync)
-        name = f"chain[{steps[0].name}..{steps[-1].name}]"
-        prog.add_memset(name + "/sync", d["sync"], 4 * n)
-        prog.add_chain(name, self.chain_cfg - SEPW_BASE, d)
+        d["sync"] = _lib.ptr(sync)       # zeroed by the launch itself (chain_reset_kernel)
+        prog.add_chain(f"chain[{steps[0].name}..{steps[-1].name}]", self.chain_cfg - SEPW_BASE, d)
 
     def flops_per_image(self) -> float:
         return 2 * 8.356e9

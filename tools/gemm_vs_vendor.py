@@ -49,6 +49,7 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sweep", action="store_true", help="also time every candidate tile config of each GEMM")
     a = ap.parse_args(argv)
     from kdl.engine import registry
     from kdl.engine.tuning import tuning_path
@@ -107,6 +108,15 @@ def main(argv=None) -> int:
                 except Exception as e:  # noqa: BLE001 - report, do not fail the sweep
                     row["scaled_mm_e4m3_us"] = None
                     row["scaled_mm_error"] = str(e)[:200]
+            if a.sweep:
+                sw = {}
+                with torch.cuda.stream(eng.stream):
+                    for split, cfg in st.layer.variants(None):
+                        sw[cfg] = round(_time(lambda: eng._emit_conv(None, st, B, split=split, cfg=cfg),
+                                              a.iters, a.reps), 2)
+                torch.cuda.synchronize()
+                row["tuned_cfg"] = st.layer.cfg
+                row["sweep_us"] = dict(sorted(sw.items(), key=lambda kv: kv[1]))
             print(json.dumps(row), flush=True)
         del eng
         torch.cuda.empty_cache()
