@@ -73,7 +73,7 @@ class XceptionEngine(EngineBase):
         # launch (sepconv_chain_kernel, launch.h ChainArgs) with that ws tile. Alone it is 7 %
         # faster per layer (29.6 vs ~32 us at batch 32: no launch, fill or drain per layer), but
         # in the stage-pipelined bench the other stream's kernels already fill those gaps while
-        # the chain's dependency-waiting workgroups hold CUs: 20.5k vs 21.0k img/s
+        # the chain's dependency-waiting workgroups hold CUs: 21.9k vs 22.5k img/s
         # (profiles/seppool_chain_ab_r3.txt). Off by default.
         self.chain_cfg = int(os.environ.get("KDL_CHAIN", "0"))
         self.chain_min = int(os.environ.get("KDL_CHAIN_MIN", "2"))      # shortest run worth chaining
