@@ -560,7 +560,10 @@ class SignatureRunner:
     def __init__(self, sig: SignatureInfo, source: ModelSource, cfg: ServerConfig, devices: list[int]):
         self.sig, self.source, self.cfg = sig, source, cfg
         bp = cfg.batching
-        self.buckets = sorted(set(bp.allowed_batch_sizes)) if cfg.enable_batching else [bp.max_batch_size]
+        self.buckets = cfg.rank_buckets()
+        dp = cfg.scatter == "rccl" and cfg.dp_rank == 0 and sig.name == cfg.dp_signature
+        if dp:                  # one collective step serves world x a per-GPU bucket (serving/dp.py)
+            self.buckets = [b * cfg.dp_world for b in self.buckets]
         self.max_batch = self.buckets[-1]
         S = source.input_size
         item_bytes = S * S * 3 * (1 if sig.input_dtype == P.DT_UINT8 else 4)
@@ -574,7 +577,11 @@ class SignatureRunner:
         self.executors: list[_Executor] = []
         self.faults = FaultInjector()
         self.exec_group = _lib.rt().ExecGroup()     # native executors: last one out shuts the batcher
-        if devices:
+        if dp:
+            from .dp import make_executor_class
+            dev = torch.device("cuda", devices[0]) if devices else torch.device("cpu")
+            self.executors.append(make_executor_class()(self, dev, cfg.dp_world))
+        elif devices:
             for d in devices:
                 for i in range(cfg.executors_for(len(devices))):
                     self.executors.append(GPUExecutor(self, d, cfg.engine_kwargs(), index=i))

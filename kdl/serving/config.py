@@ -74,6 +74,12 @@ class ServerConfig:
     procs: int = 1
     gpu_index: int = -1
     warm_signatures: list[str] = field(default_factory=list)   # built at load, besides serving_default
+    # --scatter rccl: ONE front-end (rank 0) + one process per GPU, batches scattered / logits
+    # gathered over RCCL (serving/dp.py); host = every process ingests its own requests
+    scatter: str = "host"
+    dp_world: int = 0             # processes (GPUs) of the rccl group; 0 = every visible GPU
+    dp_rank: int = -1             # set by the launcher
+    dp_signature: str = "serving_default"
     log_format: str = "text"      # text | json (one JSON object per line, for log shippers)
     stats_log_interval_s: float = 0.0   # > 0: a "stats" log record (metrics snapshot) this often
 
@@ -85,6 +91,12 @@ class ServerConfig:
         # derived counts stop at 2 per GPU: each executor keeps a compute and a copy stream
         # busy, and a process gets GPU_MAX_HW_QUEUES = 4 hardware queues per device
         return min(2, max(1, -(-self.batching.num_batch_threads // max(1, n_devices))))
+
+    def rank_buckets(self) -> list[int]:
+        """Per-GPU graph buckets (the allowed batch sizes); the data-parallel signature's
+        batcher forms batches of world x these (--scatter rccl)."""
+        bp = self.batching
+        return sorted(set(bp.allowed_batch_sizes)) if self.enable_batching else [bp.max_batch_size]
 
     def engine_kwargs(self) -> dict:
         return {"graph": self.graph, "stages": self.stages, "lanes": self.lanes, "depth": self.exec_depth}
@@ -134,6 +146,14 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--warm_signatures", default="",
                     help="comma list of signatures whose engines / graphs are built at model load (like "
                          "TF-Serving warmup requests); serving_default always is")
+    ap.add_argument("--scatter", choices=["host", "rccl"], default="host",
+                    help="rccl: one front-end process scatters each batch over the node's GPUs and gathers "
+                         "the logits on RCCL (one process per GPU, --dp_world of them); host: every server "
+                         "process feeds its own GPU (see --procs)")
+    ap.add_argument("--dp_world", type=int, default=0, help="GPUs of the --scatter rccl group (0 = all visible)")
+    ap.add_argument("--dp_rank", type=int, default=-1, help=argparse.SUPPRESS)   # set by the rccl launcher
+    ap.add_argument("--dp_signature", default="serving_default",
+                    help="the signature served data parallel under --scatter rccl (others run on rank 0's GPU)")
     ap.add_argument("--log_format", choices=["text", "json"], default=None,
                     help="json: one JSON object per log line (env KDL_LOG_FORMAT)")
     ap.add_argument("--stats_log_interval_s", type=float, default=None,
@@ -177,6 +197,7 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         exec_depth=a.exec_depth if a.exec_depth is not None else int(env.get("KDL_EXEC_DEPTH", "2")),
                         procs=max(1, a.procs), gpu_index=a.gpu_index,
                         warm_signatures=[s for s in a.warm_signatures.split(",") if s],
+                        scatter=a.scatter, dp_world=a.dp_world, dp_rank=a.dp_rank, dp_signature=a.dp_signature,
                         log_format=a.log_format or env.get("KDL_LOG_FORMAT", "text"),
                         stats_log_interval_s=(a.stats_log_interval_s if a.stats_log_interval_s is not None
                                               else float(env.get("KDL_STATS_LOG_INTERVAL_S", "0"))))

@@ -30,6 +30,16 @@ def list_versions(base: Path) -> list[int]:
     return sorted(int(p.name) for p in base.iterdir() if p.is_dir() and p.name.isdigit())
 
 
+def latest_version_source(cfg: ServerConfig):
+    """The ModelSource of the version the manager's initial load would serve (the rccl group's
+    rank 0 hands it to the followers before serving: serving/dp.py)."""
+    base = Path(cfg.model_base_path)
+    versions = list_versions(base) or ([1] if cfg.synthetic else [])
+    if not versions:
+        raise FileNotFoundError(f"no versions under {base} (use --synthetic_model for random weights)")
+    return load_version_dir(base / str(versions[-1]), synthetic=cfg.synthetic)
+
+
 class ModelManager:
     def __init__(self, cfg: ServerConfig):
         self.cfg = cfg

@@ -65,6 +65,64 @@ class ModelServer:
         self.manager.close()
 
 
+def _supervise(kids: list, stop_first: list | None = None) -> int:
+    """Forward SIGTERM / SIGINT (to ``stop_first`` only, when given: the rccl group's rank 0,
+    whose stop broadcast ends the followers), stop the rest when one child dies, and exit with
+    the first failing child's status."""
+    stopping = threading.Event()
+    targets = stop_first if stop_first is not None else kids
+
+    def forward(signum, _frame):
+        stopping.set()
+        for k in targets:
+            if k.poll() is None:
+                k.send_signal(signum)
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(sig, forward)
+    rc = 0
+    while True:
+        dead = [k for k in kids if k.poll() is not None]
+        if dead or stopping.is_set():
+            rc = next((k.returncode for k in dead if k.returncode), 0)
+            break
+        time.sleep(0.2)
+    if stop_first is not None:
+        for k in stop_first:
+            if k.poll() is None:
+                k.terminate()
+        deadline = time.time() + 30
+        while time.time() < deadline and any(k.poll() is None for k in kids):
+            time.sleep(0.2)
+    for k in kids:
+        if k.poll() is None:
+            k.terminate() if stop_first is None else k.kill()
+    for k in kids:
+        try:
+            k.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            k.kill()
+    return rc or next((k.returncode for k in kids if k.returncode and k.returncode > 0), 0)
+
+
+def launch_dp(argv: list[str], cfg: ServerConfig) -> int:
+    """``--scatter rccl``: rank 0 (this node's one front-end) + a follower per further GPU in
+    one torch.distributed group on 127.0.0.1 (serving/dp.py)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    base = [a for a in argv if not a.startswith(("--dp_rank", "--dp_world", "--procs", "--gpu_index"))]
+    kids = []
+    for r in range(cfg.dp_world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE=str(cfg.dp_world), LOCAL_RANK=str(r))
+        kids.append(subprocess.Popen([sys.executable, "-m", "kdl.serving", *base, f"--dp_world={cfg.dp_world}",
+                                      f"--dp_rank={r}"], env=env))
+    log.info("kdl model server: rccl data-parallel group of %d (pids %s), front-end = rank 0", cfg.dp_world,
+             [k.pid for k in kids])
+    return _supervise(kids, stop_first=kids[:1])
+
+
 def launch_procs(argv: list[str], cfg: ServerConfig) -> int:
     """``--procs N``: one server process per GPU on this node, all on the same gRPC / REST ports
     (SO_REUSEPORT: the kernel spreads client connections over them). The launcher itself never
@@ -77,38 +135,33 @@ def launch_procs(argv: list[str], cfg: ServerConfig) -> int:
             for i in range(cfg.procs)]
     log.info("kdl model server: %d processes (pids %s) sharing gRPC :%d / REST :%d", cfg.procs,
              [k.pid for k in kids], cfg.port, cfg.rest_api_port)
-    stopping = threading.Event()
-
-    def forward(signum, _frame):
-        stopping.set()
-        for k in kids:
-            if k.poll() is None:
-                k.send_signal(signum)
-    for sig in (signal.SIGINT, signal.SIGTERM):
-        signal.signal(sig, forward)
-    rc = 0
-    while True:
-        dead = [k for k in kids if k.poll() is not None]
-        if dead or stopping.is_set():
-            rc = next((k.returncode for k in dead if k.returncode), 0)
-            break
-        time.sleep(0.2)
-    for k in kids:
-        if k.poll() is None:
-            k.terminate()
-    for k in kids:
-        try:
-            k.wait(timeout=30)
-        except subprocess.TimeoutExpired:
-            k.kill()
-    return rc
+    return _supervise(kids)
 
 
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     cfg = config_from_args(argv)
     setup_logging(cfg.log_format)
-    if cfg.procs > 1:
+    if cfg.scatter == "rccl":
+        import torch
+        if cfg.dp_world <= 0:
+            cfg.dp_world = max(1, torch.cuda.device_count()) if cfg.device != "cpu" else 1
+        if cfg.dp_rank < 0:
+            return launch_dp(argv, cfg)
+        from . import dp
+        if cfg.dp_rank > 0:
+            return dp.follow(cfg, cfg.dp_rank, cfg.dp_world)
+        # rank 0: the front-end. Load the model once, hand it to the group (C1), then serve
+        # with the dp signature's batcher feeding collective steps; no hot reload (the
+        # followers' engines are built once)
+        dev = dp.init_group(cfg, 0, cfg.dp_world)
+        cfg.gpu_index = dev.index if dev.type == "cuda" else -1
+        cfg.file_system_poll_wait_seconds = 0
+        if cfg.dp_signature not in cfg.warm_signatures:
+            cfg.warm_signatures.append(cfg.dp_signature)
+        from .model_repo import latest_version_source
+        dp.share_source(latest_version_source(cfg), dev)
+    elif cfg.procs > 1:
         return launch_procs(argv, cfg)
     srv = ModelServer(cfg).start(block_until_loaded=False)
     if cfg.stats_log_interval_s > 0:

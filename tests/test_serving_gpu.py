@@ -213,3 +213,54 @@ def test_native_and_python_executors_agree_bit_for_bit(tmp_path, monkeypatch):
         finally:
             srv.stop(0)
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_rccl_scatter_server_world1(tmp_path):
+    """``--scatter rccl`` on the GPU: the launcher, rank 0's front-end, the model handed over by
+    broadcast (C1), every batch scattered (C2) into the engine's static input and the logits
+    gathered (C3) over RCCL -- world size 1 on this one-GPU box (the 8-GPU group is the same
+    code; tests/test_dp_serving.py runs two ranks over gloo)."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    base = tmp_path / "clothing-model"
+    (base / "1").mkdir(parents=True)
+    (base / "1" / "synthetic.json").write_text('{"seed": 0}')
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    logf = open(tmp_path / "srv.log", "w")
+    p = subprocess.Popen([sys.executable, "-m", "kdl.serving", "--scatter=rccl", "--dp_world=1", f"--port={port}",
+                          "--rest_api_port=0", f"--model_base_path={base}", "--host=127.0.0.1",
+                          "--allowed_batch_sizes=1,2,4,8"], cwd=str(root), stdout=logf, stderr=subprocess.STDOUT,
+                         env=dict(os.environ, PYTHONPATH=str(root)), start_new_session=True)
+    try:
+        deadline, ok = time.time() + 100, False
+        while time.time() < deadline and not ok and p.poll() is None:
+            try:
+                ch = grpc.insecure_channel(f"127.0.0.1:{port}")
+                ok = ch.unary_unary("/grpc.health.v1.Health/Check")(b"", timeout=5) == b"\x08\x01"
+                ch.close()
+            except grpc.RpcError:
+                time.sleep(0.5)
+        assert ok, (tmp_path / "srv.log").read_text()[-3000:]
+        rng = np.random.default_rng(1)
+        u8 = rng.integers(0, 256, (3, 299, 299, 3), dtype=np.uint8)
+        x = u8.astype(np.float32) / 127.5 - 1.0
+        stub = PredictionStub(grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", -1)]))
+        r = stub.Predict(make_request(x), timeout=60)
+        got = np.asarray(r.outputs["dense_7"].float_val, np.float32).reshape(3, 10)
+        ref = X.xception_forward(X.init_params(seed=0), torch.from_numpy(x)).numpy()
+        assert np.abs(got - ref).max() < 0.05 * np.abs(ref).max()
+        assert "rccl data-parallel group of 1" in (tmp_path / "srv.log").read_text()
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+        logf.close()
