@@ -57,7 +57,10 @@ struct WsSmem {
 // One BM x BN output tile of a fused separable conv: the whole body of sepconv_ws_kernel,
 // also run per work item by the persistent chain kernel below (CHAIN: write-through sc1
 // stores of the output and the caller publishes the tile; residual read after its acquire).
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, bool CHAIN>
+// ABL (timing ablation, id 27, never a candidate; wrong values): 1 = every band glds reads
+// 1 KiB contiguous (8 full lines) instead of 64 pixels x 16 B (64 lines) -- the same loads and
+// bytes, so the counted-vmcnt protocol is untouched, but 8x fewer lines for the TA
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, bool CHAIN, int ABL = 0>
 __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, uint8_t* smem) {
   constexpr int NT = 512;
   constexpr int BM = 16 * FM, BN = 64 * FN;
@@ -135,6 +138,8 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
       long p = P0 + slot;
       p = p < 0 ? 0 : (p >= NPIX ? NPIX - 1 : p);
       xsrc[i] = slot < NS ? (const uint8_t*)(a.x + p * a.ldx + q * 8) : sepw_zeros;
+      if constexpr (ABL & 1)
+        xsrc[i] = (const uint8_t*)(a.x + (long)max(P0, 0L) * a.ldx) + (i * 64 + lane) * 16;
     }
     // stages past the end (the branch-free loop keeps issuing) re-load the last one (a scalar
     // clamp; a per-lane select to a zero block cost more VALU than the drain it saves)
@@ -369,14 +374,14 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   }
 }
 
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU>
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0>
 __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[WsSmem<FM, FN, STAGES, XB>::BYTES];
   constexpr int BM = 16 * FM, BN = 64 * FN;
   const int nN = (a.NF * 16) / BN;
   const int nM = (a.M + BM - 1) / BM;
   const int wg = xcd_remap(blockIdx.x, nM * nN);
-  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, false>(a, wg / nN, wg % nN, smem);
+  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, false, ABL>(a, wg / nN, wg % nN, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -465,12 +470,14 @@ __global__ __launch_bounds__(512) void sepconv_chain_kernel(ChainArgs c) {
   X(23, 6, 6, 5, 9)         \
   X(24, 6, 6, 5, 11)        \
   X(25, 6, 6, 5, 16)        \
-  X(26, 4, 6, 5, 8)
+  X(26, 4, 6, 5, 8)          \
+  X(27, 6, 6, 5, 9)
 
 // id 7: s_memtime stamping variant (tools/stamps.py; never tuned); ids 23-26 = 0, 2, 3, 5
 // walking K from a per-M-tile rotated start
 constexpr bool sepw_stamp(int id) { return id == 7; }
-constexpr bool sepw_krot(int id) { return id >= 23 && id <= 26; }
+constexpr bool sepw_krot(int id) { return id >= 23 && id <= 27; }
+constexpr int sepw_abl(int id) { return id == 27 ? 1 : 0; }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }
 
@@ -510,10 +517,10 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
 #define KDL_SWCASE(id, fm, fn, st, xb)                                                                \
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), true>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), true, sepw_abl(id)>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     else                                                                                            \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), false>), dim3(grid), \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), false, sepw_abl(id)>), dim3(grid), \
                          dim3(th), 0, s, a);                                                        \
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)
@@ -526,7 +533,8 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
 #define KDL_CHAIN_CONFIGS(X) \
   X(23, 6, 6, 5, 9)          \
   X(24, 6, 6, 5, 11)         \
-  X(26, 4, 6, 5, 8)
+  X(26, 4, 6, 5, 8)          \
+  X(27, 6, 6, 5, 9)
 
 static int chain_bm(int cfg) {
   switch (cfg) {
