@@ -1,8 +1,10 @@
 """``python -m kdl.cli <command>``: TF-free model tooling.
 
   show <saved_model_dir>                     saved_model_cli-style signature dump (guide.md:202)
-  convert-savedmodel <saved_model_dir> <out> SavedModel -> kdl_params.safetensors (the Keras fp32
-                                             variables, unfolded) + kdl_model.json (head, signatures)
+  convert-savedmodel <saved_model_dir> <out> SavedModel -> kdl_params.safetensors (BN folded into
+                                             the conv kernels, kernels bf16: kdl.ingest.fold;
+                                             --keep-bn: the Keras fp32 variables as they are)
+                                             + kdl_model.json (head, signatures)
   make-synthetic <repo>/<version> [--seed] [--model xception|resnet50|vit_b16|efficientnet_b7]
                                              random-init weights of the exact architecture (Xception:
                                              a SavedModel; other families: torchvision-layout safetensors)
@@ -24,6 +26,7 @@ def main(argv=None) -> int:
     c = sub.add_parser("convert-savedmodel")
     c.add_argument("src")
     c.add_argument("dst")
+    c.add_argument("--keep-bn", action="store_true", help="write the unfolded fp32 variables")
     m = sub.add_parser("make-synthetic")
     m.add_argument("dst")
     m.add_argument("--seed", type=int, default=0)
@@ -44,11 +47,15 @@ def main(argv=None) -> int:
         params, head = to_xception_params(sm.variables())
         out = Path(a.dst)
         out.mkdir(parents=True, exist_ok=True)
+        if not a.keep_bn:
+            from .ingest.fold import fold_xception
+            params = fold_xception(params)
         save_file({k: v.contiguous() for k, v in params.items()}, str(out / "kdl_params.safetensors"))
         sigs = {n: {"input_key": next(iter(sg.inputs)), "input_dtype": next(iter(sg.inputs.values())).dtype,
                     "output_key": next(iter(sg.outputs))} for n, sg in sm.signatures.items() if sg.inputs}
         meta = {"head": {"hidden": head.hidden, "out": head.out, "hidden_units": head.hidden_units,
-                         "classes": head.classes}, "signatures": sigs, "source": str(a.src)}
+                         "classes": head.classes}, "signatures": sigs, "source": str(a.src),
+                "bn_folded": not a.keep_bn}
         (out / "kdl_model.json").write_text(json.dumps(meta, indent=1))
         print(f"wrote {out}/kdl_params.safetensors ({len(params)} tensors)")
     elif a.cmd == "make-synthetic":

@@ -207,6 +207,8 @@ def _sep(x, p, op: Sep):
 
 
 def _bn(x, p, name, calibrate_bn):
+    if f"{name}/gamma" not in p:        # folded artifact: the kernel carries the scale
+        return x + p[f"{name}/beta"][None, :, None, None]
     if calibrate_bn:
         mean = x.mean(dim=(0, 2, 3))
         var = x.var(dim=(0, 2, 3), unbiased=False)

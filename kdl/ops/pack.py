@@ -18,6 +18,9 @@ def round_up(x: int, m: int) -> int:
 
 
 def bn_scale_shift(p: dict, bn: str, eps: float = KERAS_BN_EPS):
+    if f"{bn}/gamma" not in p:          # BN already folded into the kernel (kdl.ingest.fold)
+        b = p[f"{bn}/beta"].double()
+        return torch.ones_like(b), b
     g, b = p[f"{bn}/gamma"].double(), p[f"{bn}/beta"].double()
     m, v = p[f"{bn}/moving_mean"].double(), p[f"{bn}/moving_variance"].double()
     s = g / torch.sqrt(v + eps)

@@ -112,7 +112,8 @@ def load_version_dir(path: Path, synthetic: bool = False) -> ModelSource:
         origin = "saved_model"
     elif (path / "kdl_params.safetensors").exists():
         from safetensors.torch import load_file
-        params = load_file(str(path / "kdl_params.safetensors"))
+        from ..ingest.fold import unpack
+        params = unpack(load_file(str(path / "kdl_params.safetensors")))
         meta = json.loads((path / "kdl_model.json").read_text()) if (path / "kdl_model.json").exists() else {}
         if meta.get("family", "xception") != "xception":
             return _family_source(meta["family"], params, 0, "kdl_safetensors")
