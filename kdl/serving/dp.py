@@ -39,15 +39,20 @@ log = logging.getLogger("kdl.serving")
 
 
 def init_group(cfg, rank: int, world: int) -> torch.device:
-    """Join the node's process group; returns this rank's device."""
+    """Join the node's process group; returns this rank's device. Collectives time out after
+    KDL_DP_TIMEOUT_S (default 120 s): a rank that died fails rank 0's batches (the executor
+    then marks itself unhealthy) instead of hanging the front-end."""
+    from datetime import timedelta
+    import os
+    timeout = timedelta(seconds=float(os.environ.get("KDL_DP_TIMEOUT_S", "120")))
     use_gpu = cfg.device != "cpu" and torch.cuda.device_count() > 0
     if use_gpu:
         dev = torch.device("cuda", rank % torch.cuda.device_count())
         torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=timeout)
     else:
         dev = torch.device("cpu")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timeout)
     return dev
 
 
