@@ -173,8 +173,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
   X(7, 4, 4, 2, 4, 2)     \
   X(8, 5, 2, 2, 4, 2)     \
   X(9, 5, 3, 2, 4, 2)     \
-  X(10, 5, 4, 2, 4, 2)
-// 8-10: 160-row tiles, whole waves of 256 CUs at the ViT-B/16 token count (gemm_pipe.hip 45-47)
+  X(10, 5, 4, 2, 4, 2)     \
+  X(11, 4, 4, 2, 4, 3)     \
+  X(12, 5, 2, 2, 4, 3)     \
+  X(13, 4, 2, 2, 4, 3)     \
+  X(14, 5, 2, 2, 4, 4)     \
+  X(15, 4, 2, 2, 4, 4)
+// 8-10: 160-row tiles, whole waves of 256 CUs at the ViT-B/16 token count (gemm_pipe.hip 45-47);
+// 11-15: 3-4 stage rings of the large tiles (2 stages leave one k-step of load latency exposed)
 
 int gemm_f8_config(int cfg, int* bm, int* bn, int* threads) {
   switch (cfg) {

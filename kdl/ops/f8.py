@@ -16,7 +16,9 @@ E4M3_MAX = 448.0
 # (FM, FN, WGM, WGN, STAGES) of KDL_F8_CONFIGS in gemm_f8.hip
 F8_CONFIGS = {0: (4, 4, 2, 2, 2), 1: (4, 4, 2, 2, 3), 2: (2, 4, 2, 2, 3), 3: (4, 2, 2, 4, 2),
               4: (3, 3, 2, 4, 2), 5: (6, 3, 2, 4, 2), 6: (3, 6, 2, 4, 2), 7: (4, 4, 2, 4, 2),
-              8: (5, 2, 2, 4, 2), 9: (5, 3, 2, 4, 2), 10: (5, 4, 2, 4, 2)}
+              8: (5, 2, 2, 4, 2), 9: (5, 3, 2, 4, 2), 10: (5, 4, 2, 4, 2),
+              11: (4, 4, 2, 4, 3), 12: (5, 2, 2, 4, 3), 13: (4, 2, 2, 4, 3), 14: (5, 2, 2, 4, 4),
+              15: (4, 2, 2, 4, 4)}
 
 
 def f8_tile(cfg: int) -> tuple[int, int]:
