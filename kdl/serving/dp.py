@@ -161,6 +161,8 @@ def make_executor_class():
             self.dev, self.world = dev, world
 
         def setup(self):
+            if self.dev.type == "cuda":
+                torch.cuda.set_device(self.dev)   # the current device is per thread
             r = self.runner
             src = r.source
             u8 = r.sig.input_dtype == P.DT_UINT8
