@@ -26,15 +26,9 @@ __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-// ABL: timing-ablation bits (tools/kbench.py --cfgs; never autotune candidates):
-//   1 no MFMA, 2 no LDS-DMA in the k-loop, 4 no global stores, 8 no LDS fragment reads,
-//   16 A fragments DMA'd from a contiguous 1 KiB source (same bytes, B-like full-line
-//   access instead of 16 rows x 64 B; wrong values, timing only), 32 no A DMA,
-//   64 no B DMA, 128 rotate the k order per workgroup (a real variant: workgroups
-//   sharing the weights start at different k-steps instead of all requesting the same
-//   weight fragments at once)
-// DT: element type (common.h Elt): 0 bf16, 1 fp16
-template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int ABL = 0, int DT = 0>
+// DT: element type (common.h Elt): 0 bf16, 1 fp16. (Round 2's timing ablations of this
+// kernel -- no MFMA / no DMA / no stores / contiguous A -- are in profiles/kernel_ablations_r2.txt.)
+template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int DT = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs a) {
   using E = Elt<DT>;
   constexpr int NW = WGM * WGN;
@@ -96,7 +90,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   // Issue stage t (k32 steps t*KSUB .. t*KSUB+KSUB-1). A sub-step past the end
   // of K re-issues the stage's first sub-step into its own slot (its MFMAs are
   // skipped), so every stage has exactly L*KSUB DMAs for the counted vmcnt.
-  const int krot = (ABL & 128) ? (int)(blockIdx.x % (unsigned)KT32) : a.krot ? (mi * 7) % KT32 : 0;
+  const int krot = a.krot ? (mi * 7) % KT32 : 0;
   auto issue = [&](int t, int buf) {
 #pragma unroll
     for (int ks = 0; ks < KSUB; ++ks) {
@@ -116,14 +110,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
 #pragma unroll
       for (int i = 0; i < L; ++i) {
         const int f = min(wave + i * NW, FR - 1);
-        if (f < AF) {
-          if constexpr (ABL & 32) {
-          } else if constexpr (ABL & 16)
-            glds16(a.x + ((long)min(m0 / 16 + f, a.M / 16 - 1) * KT32 + k32) * 512 + lane * 8, base + f * 1024);
-          else
-            glds16(a.x + src[i] + koff_a, base + f * 1024);
-        }
-        else if constexpr (!(ABL & 64)) glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
+        if (f < AF) glds16(a.x + src[i] + koff_a, base + f * 1024);
+        else glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
       }
     }
   };
@@ -144,38 +132,24 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     if (after >= 2) wait_vm_barrier<2 * L * KSUB>();
     else if (after == 1) wait_vm_barrier<L * KSUB>();
     else wait_vm_barrier<0>();
-    if (!(ABL & 2) && t + STAGES - 1 < KT) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+    if (t + STAGES - 1 < KT) issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
 #pragma unroll
     for (int ks = 0; ks < KSUB; ++ks) {
       if (KSUB > 1 && t * KSUB + ks >= KT32) break;
       const uint8_t* st = smem + (t % STAGES) * STAGE + ks * FR * 1024 + lane * 16;
       s16x8 af[FM], bf[FN];
-      if constexpr (ABL & 8) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = (s16x8){(short)(t + i), 1, 2, 3, 4, 5, 6, (short)lane};
+      for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bf[j] = (s16x8){(short)(t + j), 3, 2, 1, 4, 5, 6, (short)ks};
-      } else {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
-      }
+      for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
       // raise this wave's issue priority while it streams MFMAs (guide §5 T-setprio:
       // the other waves' glds issue / barrier arrival no longer interleave into the
       // MFMA run)
       __builtin_amdgcn_s_setprio(1);
-      if constexpr (ABL & 1) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j][0] += __uint_as_float((uint32_t)af[i][0] ^ (uint32_t)bf[j][1]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = E::mfma(bf[j], af[i], acc[i][j]);
-      }
+        for (int j = 0; j < FN; ++j) acc[i][j] = E::mfma(bf[j], af[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
   }
@@ -203,13 +177,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   for (int c = tid; c < BM * CPR; c += 64 * NW) {
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
-    if (m < mend && n < a.nstore) {
-      if constexpr (ABL & 4) {
-        if (smem[r * CS + cc * 16] == 0x7f && smem[r * CS + cc * 16 + 1] == 0x7f) a.y[0] = 1;   // keep the tile live
-      } else {
-        epi_store<DT>(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
-      }
-    }
+    if (m < mend && n < a.nstore) epi_store<DT>(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
   }
 }
 
@@ -245,38 +213,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   X(45, 5, 2, 2, 4, 3, 1)   \
   X(46, 5, 3, 2, 4, 3, 1)   \
   X(47, 5, 4, 2, 4, 3, 1)
-// 45-47: 160-row tiles (ids after the ablations). At the ViT-B/16 shapes (M = 32 x 197 =
+// 45-47: 160-row tiles (256x256 / 256x192 / 192x256 tiles were tried in round 3 and lost:
+// profiles/vit_gemm_tiles256_r3.txt). At the ViT-B/16 shapes (M = 32 x 197 =
 // 6304 rows) they fill 256 CUs in whole waves: out_proj / mlp.3 (N 768) 160x128 -> 240
 // tiles; QKV (N 2304) 160x192 -> 480; mlp.0 (N 3072) 160x256 -> 480 (vs 192x192: 396 / 528)
 
-// timing ablations of id 9 (ABL bits above), ids 27..44
-#define KDL_PIPE_ABL(X) \
-  X(27, 6, 3, 2, 4, 3, 1, 1) \
-  X(28, 6, 3, 2, 4, 3, 1, 2) \
-  X(29, 6, 3, 2, 4, 3, 1, 4) \
-  X(30, 6, 3, 2, 4, 3, 1, 8) \
-  X(31, 6, 3, 2, 4, 3, 1, 15) \
-  X(32, 6, 3, 2, 4, 3, 1, 16) \
-  X(33, 6, 3, 2, 4, 3, 1, 20) \
-  X(34, 6, 3, 2, 4, 3, 1, 13) \
-  X(35, 6, 3, 2, 4, 5, 1, 13) \
-  X(36, 6, 3, 2, 4, 5, 1, 0)  \
-  X(37, 6, 3, 2, 4, 2, 2, 13) \
-  X(38, 6, 3, 2, 4, 2, 2, 0)  \
-  X(39, 6, 3, 2, 4, 3, 2, 13) \
-  X(40, 6, 3, 2, 4, 3, 2, 0)  \
-  X(41, 6, 3, 2, 4, 3, 1, 45) \
-  X(42, 6, 3, 2, 4, 3, 1, 77) \
-  X(43, 6, 3, 2, 4, 3, 1, 141) \
-  X(44, 6, 3, 2, 4, 3, 1, 128)
-
-template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int ABL = 0, int DT = 0>
+template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int DT = 0>
 static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
   if (a.wimg && (a.M != a.B * a.OH * a.OW || a.B <= 0)) return hipErrorInvalidValue;
   const int nM = a.wimg ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, ABL, DT>), dim3(nM * nN),
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT>), dim3(nM * nN),
                      dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();
 }
@@ -285,20 +233,9 @@ template <int MODE, int DT>
 static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   switch (cfg) {
 #define KDL_PCASE(id, fm, fn, wgm, wgn, st, ks) \
-  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, 0, DT>(a, s);
+  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, DT>(a, s);
     KDL_PIPE_CONFIGS(KDL_PCASE)
 #undef KDL_PCASE
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// timing ablations: pointwise mode, bf16 only
-static hipError_t launch_pipe_ablation(int cfg, const ConvGemmArgs& a, hipStream_t s) {
-  switch (cfg) {
-#define KDL_PACASE(id, fm, fn, wgm, wgn, st, ks, abl) \
-  case id: return launch_pipe_cfg<0, fm, fn, wgm, wgn, st, ks, abl, 0>(a, s);
-    KDL_PIPE_ABL(KDL_PACASE)
-#undef KDL_PACASE
     default: return hipErrorInvalidValue;
   }
 }
@@ -308,7 +245,6 @@ hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& args, hipStream_t s)
   static const int env_krot = [] { const char* e = getenv("KDL_PIPE_KROT"); return e ? atoi(e) : -1; }();
   ConvGemmArgs a = args;
   if (env_krot >= 0) a.krot = env_krot;
-  if (cfg >= 27 && cfg <= 44) return mode == 0 && a.dt == 0 ? launch_pipe_ablation(cfg, a, s) : hipErrorInvalidValue;
   if (mode == 0) return a.dt ? launch_pipe_mode<0, 1>(cfg, a, s) : launch_pipe_mode<0, 0>(cfg, a, s);
   if (mode == 1) return a.dt ? launch_pipe_mode<1, 1>(cfg, a, s) : launch_pipe_mode<1, 0>(cfg, a, s);
   return hipErrorInvalidValue;
@@ -320,10 +256,6 @@ int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads) {
   case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
     KDL_PIPE_CONFIGS(KDL_PINFO)
 #undef KDL_PINFO
-#define KDL_PAINFO(id, fm, fn, wgm, wgn, st, ks, abl) \
-  case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
-    KDL_PIPE_ABL(KDL_PAINFO)
-#undef KDL_PAINFO
     default: return -1;
   }
 }

@@ -33,11 +33,6 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            32: (4, 2, 2, 4), 33: (4, 4, 2, 2), 34: (3, 3, 2, 4), 35: (4, 4, 2, 2),
            36: (2, 4, 2, 2), 37: (4, 2, 2, 2), 38: (6, 3, 2, 4), 39: (3, 6, 2, 4),
            40: (3, 3, 2, 4), 41: (4, 2, 2, 4), 42: (6, 3, 2, 4),
-           # timing ablations of 25 (gemm_pipe.hip KDL_PIPE_ABL; never candidates)
-           43: (6, 3, 2, 4), 44: (6, 3, 2, 4), 45: (6, 3, 2, 4), 46: (6, 3, 2, 4), 47: (6, 3, 2, 4),
-           48: (6, 3, 2, 4), 49: (6, 3, 2, 4), 50: (6, 3, 2, 4), 51: (6, 3, 2, 4),
-           52: (6, 3, 2, 4), 53: (6, 3, 2, 4), 54: (6, 3, 2, 4), 55: (6, 3, 2, 4), 56: (6, 3, 2, 4),
-           57: (6, 3, 2, 4), 58: (6, 3, 2, 4), 59: (6, 3, 2, 4), 60: (6, 3, 2, 4),
            # 160-row LDS-DMA tiles (gemm_pipe.hip ids 45-47): whole waves at the ViT token counts
            61: (5, 2, 2, 4), 62: (5, 3, 2, 4), 63: (5, 4, 2, 4),
            # warp-specialized fused separable conv (sepconv_ws.hip, KDL_SEPW_CONFIGS): (FM, FN, 1, 4);
@@ -84,8 +79,8 @@ SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
            143: 9, 144: 11, 145: 16, 146: 8, 147: 9}
 # ws configs with a chained (multi-layer, one launch) variant: sepconv_ws.hip KDL_CHAIN_CONFIGS
 CHAIN_CONFIGS = (143, 144, 146)
-# never autotune candidates: gemm_pipe timing ablations (KDL_PIPE_ABL), the ws stamping build
-ABLATION_IDS = frozenset(list(range(43, 61)) + [127, 147] + list(S2DWP))
+# never autotune candidates: the ws stamping build and band ablation, the pooled sepconv (seppool only)
+ABLATION_IDS = frozenset([127, 147] + list(S2DWP))
 
 
 def s2dp_smem(cfg: int, K: int) -> int:
