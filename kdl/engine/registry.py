@@ -45,7 +45,9 @@ def _resnet50(dtype: str = "fp16"):
                      lambda seed=0: R.init_params(seed=seed),
                      lambda p, max_batch, device, **kw: ResNetEngine(p, max_batch=max_batch, device=device,
                                                                      dtype=dtype, **kw),
-                     R.resnet_forward, dtype=dtype, tuning="resnet50", stage_cut="layer3.1.conv3")
+                     # three stages (3 compute streams): +1.3-1.9 % over the round-2 cut after layer3.1
+                     # (profiles/stages3_ab_r3.txt)
+                     R.resnet_forward, dtype=dtype, tuning="resnet50", stage_cut="layer2.1.conv3,layer3.3.conv3")
 
 
 def _vit_b16():

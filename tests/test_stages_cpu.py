@@ -165,10 +165,13 @@ def test_resnet_cut_inside_stage_privatises_shared_buffers():
     e = FR(p)
     e._build(p)
     from kdl.engine import registry
-    sp = _analyse(e.steps, registry.get("resnet50").stage_cut)
+    sp = _analyse(e.steps, "layer3.1.conv3")
     assert len(sp.boundary) == 1
     # layer3's pad / mid buffers are used on both sides of a layer3.1 cut
     assert "pad14_256#s1" in sp.aliases and "mid14_256#s1" in sp.aliases
+    # the default: three stages (cuts after layer2.1 and layer3.3), two parity-buffered boundaries
+    sp3 = _analyse(e.steps, registry.get("resnet50").stage_cut)
+    assert len(sp3.ranges) == 3 and sorted(sp3.boundary) == ["out14x1024_1", "out28x512_1"]
 
 
 def test_xception_residual_conv_carries_the_pool():
