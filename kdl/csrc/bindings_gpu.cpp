@@ -151,6 +151,17 @@ GemmF8Args f8_args(const py::dict& d) {
   a.krot = I(d, "krot");
   return a;
 }
+BlasLtArgs blaslt_args(const py::dict& d) {
+  BlasLtArgs a{};
+  a.x = P<const void>(d, "x"); a.w = P<const void>(d, "w"); a.y = P<void>(d, "y");
+  a.res = P<const void>(d, "res"); a.bias = P<const float>(d, "bias");
+  a.M = I(d, "M"); a.N = I(d, "N"); a.K = I(d, "K");
+  a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
+  a.relu = I(d, "relu"); a.dt = I(d, "dt"); a.algo = I(d, "algo");
+  a.wscale = P<const float>(d, "wscale");
+  return a;
+}
+
 FcMfmaArgs fcm_args(const py::dict& d) {
   FcMfmaArgs a{};
   a.xb = P<const uint16_t>(d, "xb"); a.wp = P<const uint16_t>(d, "wp"); a.bias = P<const float>(d, "bias");
@@ -229,6 +240,18 @@ PYBIND11_MODULE(_C, m) {
     const auto a = conv_args(d);
     py::gil_scoped_release nogil;
     chk(conv_gemm(mode, cfg, a, S(s)), "conv_gemm");
+  });
+  // hipBLASLt GEMM node, eager (tests); returns the heuristic's algorithm count
+  m.def("blaslt", [](py::dict d, uintptr_t s) {
+    auto a = blaslt_args(d);
+    const int n = blaslt_prepare(a);
+    py::gil_scoped_release nogil;
+    chk(blaslt_run(static_cast<const BlasLtArgs&>(a), S(s)), "blaslt");
+    return n;
+  });
+  m.def("blaslt_num_algos", [](py::dict d) {
+    auto a = blaslt_args(d);
+    return blaslt_prepare(a);
   });
   m.def("conv_gemm_config", [](int cfg) {
     int bm = 0, bn = 0, th = 0;
@@ -398,6 +421,12 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
       .def("add_conv_gemm", [](Program& p, const std::string& name, int mode, int cfg, py::dict d) {
         Op op; op.kind = OP_CONV_GEMM; op.name = name; op.mode = mode; op.cfg = cfg; op.g = conv_args(d);
+        p.add(op);
+      })
+      .def("add_blaslt", [](Program& p, const std::string& name, py::dict d) {
+        Op op; op.kind = OP_BLASLT; op.name = name; op.bl = blaslt_args(d);
+        op.cfg = op.bl.algo;
+        blaslt_prepare(op.bl);
         p.add(op);
       })
       .def("add_chain", [](Program& p, const std::string& name, int cfg, py::dict d) {

@@ -17,7 +17,7 @@ from pathlib import Path
 import torch
 
 from ..ops import _lib
-from ..ops.conv import MODE_DW, ConvGemmLayer
+from ..ops.conv import MODE_DW, ConvGemmLayer, is_blaslt
 
 
 @dataclass
@@ -253,6 +253,8 @@ class EngineBase:
             if v is None:
                 continue
             split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
-            if cfg in s.layer.candidates and (not split or getattr(s.layer, "mode", -1) == MODE_DW):
+            ok = cfg in s.layer.candidates or (is_blaslt(cfg) and (getattr(s.layer, "w_plain", None) is not None
+                                                                   or getattr(s.layer, "w8_plain", None) is not None))
+            if ok and (not split or getattr(s.layer, "mode", -1) == MODE_DW):
                 s.layer.split, s.layer.cfg = split, cfg
         self.invalidate()

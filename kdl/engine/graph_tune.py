@@ -68,7 +68,7 @@ def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
 
 
 def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, margin: float = 0.002,
-               log=print, only: set | None = None, tie: str | None = None) -> dict:
+               log=print, only: set | None = None, tie: str | None = None, verbose: bool = False) -> dict:
     """``only``: challenge the incumbents with these tile configs only (e.g. newly added ids).
     ``tie``: regex; steps whose names are equal once it is replaced by '*' move together (the
     12 identical encoder layers of a ViT: one layer's few-us win sits inside the margin, the
@@ -97,6 +97,8 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
                 trial = dict(table, **{m.name: cand for m in members})
                 eng.apply_tuning(trial)
                 t = graph_time(eng, b, reps)
+                if verbose:
+                    log(f"    {cand}: {t * 1e3:.1f} us")
                 if t >= base * (1 - margin):
                     continue
                 # interleaved A/B: incumbent vs challenger, median of `confirm` rounds each
@@ -133,6 +135,7 @@ def main(argv=None) -> int:
     ap.add_argument("--start", default=None, help="starting table (default: the committed table)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--cfgs", default=None, help="comma list: only these configs challenge the table")
+    ap.add_argument("--verbose", action="store_true", help="log every challenger's graph time")
     ap.add_argument("--tie", default=None, help=r"regex, e.g. 'encoder_layer_\d+': tune matching layers together")
     a = ap.parse_args(argv)
     from . import registry
@@ -164,7 +167,7 @@ def main(argv=None) -> int:
     t0 = time.time()
     only = {int(c) for c in a.cfgs.split(",")} if a.cfgs else None
     table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only,
-                       tie=a.tie)
+                       tie=a.tie, verbose=a.verbose)
     Path(a.out).write_text(json.dumps(table, indent=1))
     print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
     return 0

@@ -63,9 +63,13 @@ class ViTEngine(EngineBase):
         if tune_file and Path(tune_file).exists():
             self.load_tuning(tune_file)
 
-    def _lin(self, name: str, w: torch.Tensor, b: torch.Tensor, relu_out: int = 0) -> ConvGemmLayer:
+    def _lin(self, name: str, w: torch.Tensor, b: torch.Tensor, relu_out: int = 0,
+             blaslt: bool = True) -> ConvGemmLayer:
+        # blaslt: hipBLASLt is a tuning candidate for the plain linears (bias, or bias + the
+        # residual as its C operand); not for mlp.0 (exact-erf GELU epilogue) or the patch
+        # embedding (writes into per-image token rows)
         lay = ConvGemmLayer(name, MODE_PW, w.double(), b.float(), cin_pad=w.shape[1], n=w.shape[0],
-                            relu_out=relu_out, device=self.device)
+                            relu_out=relu_out, device=self.device, blaslt=blaslt and relu_out != 3)
         lay.krot = 1    # K-rotated LDS-DMA GEMM: bf16 +0.6 % img/s, p50 -2.9 % (profiles/krot_ab.txt)
         return lay
 
@@ -74,7 +78,7 @@ class ViTEngine(EngineBase):
         self.ln = {}
         self.steps.append(Step("patchify", "patchify", src="input", dst="patches"))
         w = p["conv_proj.weight"].reshape(D, 3 * V.PATCH * V.PATCH)
-        self.steps.append(Step("conv", "conv_proj", self._lin("conv_proj", w, p["conv_proj.bias"]),
+        self.steps.append(Step("conv", "conv_proj", self._lin("conv_proj", w, p["conv_proj.bias"], blaslt=False),
                                "patches", "X", extra=dict(kind="patch")))
         self.cls = p["class_token"].reshape(D).float().to(dev)
         self.pos = p["encoder.pos_embedding"].reshape(self.T, D).float().contiguous().to(dev)
@@ -118,18 +122,18 @@ class ViTEngine(EngineBase):
         self.steps.append(Step("ln", f"{L}.ln_1", src="X", dst="Xn8", extra=dict(out_scale=sc["ln_1"])))
         self.steps.append(Step("f8", f"{L}.qkv", F8Linear(
             f"{L}.qkv", p[f"{L}.self_attention.in_proj_weight"], p[f"{L}.self_attention.in_proj_bias"], sc["ln_1"],
-            device=dev), "Xn8", "QKV"))
+            device=dev, blaslt=True), "Xn8", "QKV"))
         self.steps.append(Step("attn", f"{L}.attn", src="QKV", dst="A8", extra=dict(out_scale=sc["attn"])))
         self.steps.append(Step("f8", f"{L}.out_proj", F8Linear(
             f"{L}.out_proj", p[f"{L}.self_attention.out_proj.weight"], p[f"{L}.self_attention.out_proj.bias"],
-            sc["attn"], device=dev), "A8", "X", res="X"))
+            sc["attn"], device=dev, blaslt=True), "A8", "X", res="X"))
         self.steps.append(Step("ln", f"{L}.ln_2", src="X", dst="Xn8", extra=dict(out_scale=sc["ln_2"])))
         self.steps.append(Step("f8", f"{L}.mlp.0", F8Linear(
             f"{L}.mlp.0", p[f"{L}.mlp.0.weight"], p[f"{L}.mlp.0.bias"], sc["ln_2"], relu_out=3, device=dev),
             "Xn8", "Hd8", extra=dict(out_scale=sc["gelu"])))
         self.steps.append(Step("f8", f"{L}.mlp.3", F8Linear(
-            f"{L}.mlp.3", p[f"{L}.mlp.3.weight"], p[f"{L}.mlp.3.bias"], sc["gelu"], device=dev), "Hd8", "X",
-            res="X"))
+            f"{L}.mlp.3", p[f"{L}.mlp.3.weight"], p[f"{L}.mlp.3.bias"], sc["gelu"], device=dev, blaslt=True),
+            "Hd8", "X", res="X"))
 
     def _alloc(self) -> None:
         B, S, dev, D, T = self.max_batch, self.size, self.device, V.DIM, self.T

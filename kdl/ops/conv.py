@@ -77,6 +77,10 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
            135: 15, 136: 11, 137: 15, 140: 8, 141: 8, 142: 8,
            143: 9, 144: 11, 145: 16, 146: 8, 147: 9}
+# ids >= BLT_BASE: the vendor GEMM node (hipBLASLt, runtime/blaslt.cpp) for plain dense linears of
+# layers built with blaslt=True; id - BLT_BASE = rank in hipBLASLt's heuristic list for the shape
+BLT_BASE = 1000
+BLT_ALGOS = 6
 # ws configs with a chained (multi-layer, one launch) variant: sepconv_ws.hip KDL_CHAIN_CONFIGS
 CHAIN_CONFIGS = (143, 144, 146)
 # never autotune candidates: the ws stamping build and band ablation, the pooled sepconv (seppool only)
@@ -129,7 +133,13 @@ def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | No
     return False
 
 
+def is_blaslt(cfg: int) -> bool:
+    return cfg >= BLT_BASE
+
+
 def cfg_tile(cfg: int) -> tuple[int, int]:
+    if is_blaslt(cfg):          # no tile of ours: channels are stored unpadded (16-granular)
+        return 256, 16
     fm, fn, wgm, wgn = CONFIGS[cfg]
     return 16 * fm * wgm, 16 * fn * wgn
 
@@ -182,9 +192,13 @@ class ConvGemmLayer:
     def __init__(self, name: str, mode: int, w_nk: torch.Tensor, bias: torch.Tensor, *,
                  cin_pad: int, n: int, stride: int = 1, dww: torch.Tensor | None = None,
                  relu_in: bool = False, relu_out: bool | int = False, device="cuda",
-                 candidates: list[int] | None = None, dtype: torch.dtype = torch.bfloat16):
+                 candidates: list[int] | None = None, dtype: torch.dtype = torch.bfloat16,
+                 blaslt: bool = False):
         """``dtype``: element type of the activations and packed weights, bf16 (default)
-        or fp16 (MODE_PW / MODE_CONV only; ``dt`` = 1 in the launch args)."""
+        or fp16 (MODE_PW / MODE_CONV only; ``dt`` = 1 in the launch args).
+        ``blaslt``: also offer the hipBLASLt GEMM node (ids >= BLT_BASE) as a variant; only
+        for a plain stride-1 pointwise linear whose epilogue is bias (+ReLU) (+residual
+        as hipBLASLt's C operand, ReLU last) -- keeps an unpacked [N][K] weight copy."""
         assert dtype in (torch.bfloat16, torch.float16), dtype
         assert dtype == torch.bfloat16 or mode != MODE_DW, "fused separable convs are bf16-only"
         self.dtype, self.dt = dtype, int(dtype == torch.float16)
@@ -213,6 +227,11 @@ class ConvGemmLayer:
             self.dwk = pack_dw_entries(dww).to(device)
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
         self.w_ref = w_nk.to(dtype).float()
+        self.w_plain = None
+        if blaslt:
+            assert mode == MODE_PW and stride == 1 and self.relu_out in (0, 1, 2) and not relu_in, \
+                (name, "hipBLASLt node: plain linear, bias / ReLU / residual epilogues only")
+            self.w_plain = w_nk.to(dtype).to(device).contiguous()
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
         # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
         self.split = False
@@ -224,7 +243,8 @@ class ConvGemmLayer:
             return [(False, c) for c in self.candidates
                     if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))]
         if self.mode != MODE_DW:
-            return [(False, c) for c in self.candidates if c < SEP_BASE]
+            blt = [(False, BLT_BASE + i) for i in range(BLT_ALGOS)] if self.w_plain is not None else []
+            return [(False, c) for c in self.candidates if c < SEP_BASE] + blt
         return ([(False, c) for c in self.candidates
                  if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W, self.K, self.n)]
                 + [(True, c) for c in self.candidates if c < SEP_BASE])
@@ -244,6 +264,10 @@ class ConvGemmLayer:
         per-image copies of the packed weights (ConvGemmArgs.wimg; LDS-DMA GEMM configs only)."""
         split = self.split if split is None else split
         cfg = self.cfg if cfg is None else cfg
+        if is_blaslt(cfg):
+            assert pool is None and wimg is None and not split
+            self._emit_blaslt(prog, x, y, g, res, ldx, ldr, cfg, opad)
+            return
         assert pool is None or self.mode == MODE_PW or cfg in S2DWP, \
             "the pool epilogue rides a pointwise GEMM or a pooled separable config"
         C = _lib.lib()
@@ -269,6 +293,23 @@ class ConvGemmLayer:
             C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
         else:
             prog.add_conv_gemm(self.name, self.mode, cfg, ga)
+
+    def blaslt_args(self, x: int, y: int, M: int, res: int | None = None, ldx: int | None = None,
+                    ldr: int | None = None, algo: int = 0) -> dict:
+        # relu_out 1 is ReLU BEFORE the residual add, which hipBLASLt (act after C) cannot express
+        assert self.w_plain is not None, (self.name, "layer built without blaslt=True")
+        assert not (res and self.relu_out == 1), (self.name, "ReLU before the residual add")
+        return dict(x=x, w=_lib.ptr(self.w_plain), y=y, res=res, bias=_lib.ptr(self.bias), M=M, N=self.n,
+                    K=self.K, ldx=ldx if ldx is not None else self.cin_pad, ldy=self.ldy,
+                    ldr=ldr if ldr is not None else self.ldy, relu=int(self.relu_out != 0), dt=self.dt, algo=algo)
+
+    def _emit_blaslt(self, prog, x, y, g: Geometry, res, ldx, ldr, cfg: int, opad: int) -> None:
+        assert opad == 0 and g.H == g.OH and g.W == g.OW, (self.name, "hipBLASLt node: dense rows only")
+        d = self.blaslt_args(x, y, g.M, res, ldx, ldr, cfg - BLT_BASE)
+        if prog is None:
+            _lib.lib().blaslt(d, _lib.stream_ptr())
+        else:
+            prog.add_blaslt(self.name, d)
 
     def nf(self, cfg: int | None = None) -> int:
         cfg = self.cfg if cfg is None else cfg
