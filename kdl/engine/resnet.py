@@ -113,9 +113,8 @@ class ResNetEngine(EngineBase):
             out = f"out{oh}x{cout}_{ping}"      # ping-pong within a stage
             self.shapes[out] = (oh, oh, cout, 0)
             w3, b3 = _fold(p, f"{blk.prefix}.conv3.weight", f"{blk.prefix}.bn3")
-            # conv3 is a plain GEMM (bias, shortcut as C, ReLU last): hipBLASLt is a candidate
             l3 = ConvGemmLayer(f"{blk.prefix}.conv3", MODE_PW, w3, b3, cin_pad=wdt, n=cout, relu_out=2,
-                               device=dev, dtype=self.dtype, blaslt=True)
+                               device=dev, dtype=self.dtype)
             self.steps.append(Step("conv", l3.name, l3, tmid, out, res=res, geom=(oh, oh, oh, oh)))
             cur, H = out, oh
         nf = (self.classes + 15) // 16

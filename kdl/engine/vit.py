@@ -122,17 +122,17 @@ class ViTEngine(EngineBase):
         self.steps.append(Step("ln", f"{L}.ln_1", src="X", dst="Xn8", extra=dict(out_scale=sc["ln_1"])))
         self.steps.append(Step("f8", f"{L}.qkv", F8Linear(
             f"{L}.qkv", p[f"{L}.self_attention.in_proj_weight"], p[f"{L}.self_attention.in_proj_bias"], sc["ln_1"],
-            device=dev, blaslt=True), "Xn8", "QKV"))
+            device=dev), "Xn8", "QKV"))
         self.steps.append(Step("attn", f"{L}.attn", src="QKV", dst="A8", extra=dict(out_scale=sc["attn"])))
         self.steps.append(Step("f8", f"{L}.out_proj", F8Linear(
             f"{L}.out_proj", p[f"{L}.self_attention.out_proj.weight"], p[f"{L}.self_attention.out_proj.bias"],
-            sc["attn"], device=dev, blaslt=True), "A8", "X", res="X"))
+            sc["attn"], device=dev), "A8", "X", res="X"))
         self.steps.append(Step("ln", f"{L}.ln_2", src="X", dst="Xn8", extra=dict(out_scale=sc["ln_2"])))
         self.steps.append(Step("f8", f"{L}.mlp.0", F8Linear(
             f"{L}.mlp.0", p[f"{L}.mlp.0.weight"], p[f"{L}.mlp.0.bias"], sc["ln_2"], relu_out=3, device=dev),
             "Xn8", "Hd8", extra=dict(out_scale=sc["gelu"])))
         self.steps.append(Step("f8", f"{L}.mlp.3", F8Linear(
-            f"{L}.mlp.3", p[f"{L}.mlp.3.weight"], p[f"{L}.mlp.3.bias"], sc["gelu"], device=dev, blaslt=True),
+            f"{L}.mlp.3", p[f"{L}.mlp.3.weight"], p[f"{L}.mlp.3.bias"], sc["gelu"], device=dev),
             "Hd8", "X", res="X"))
 
     def _alloc(self) -> None:

@@ -102,3 +102,4 @@ def test_blaslt_e4m3_linear_matches_dequantized_reference():
         lay.emit(None, cfg=BLT_BASE + algo, x8=x8.data_ptr(), M=M, y=y.data_ptr(), res=y.data_ptr(), ldy=N)
         torch.cuda.synchronize()
         assert _rel(y, ref) < 1e-2, algo
+
