@@ -95,11 +95,17 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
                 if cand == cur:
                     continue
                 trial = dict(table, **{m.name: cand for m in members})
+                # screen against a FRESH incumbent time taken right before the challenger: a
+                # baseline measured minutes earlier drifts with the chip's clock under sustained
+                # load (measured: every challenger 4-10 % slower than a stale start, including a
+                # hipBLASLt mlp.3 that wins 5 % in bench.py), so a one-sided screen rejected all
+                eng.apply_tuning(table)
+                t_inc = graph_time(eng, b, reps)
                 eng.apply_tuning(trial)
                 t = graph_time(eng, b, reps)
                 if verbose:
-                    log(f"    {cand}: {t * 1e3:.1f} us")
-                if t >= base * (1 - margin):
+                    log(f"    {cand}: {t * 1e3:.1f} us (incumbent {t_inc * 1e3:.1f})")
+                if t >= t_inc * (1 - margin):
                     continue
                 # interleaved A/B: incumbent vs challenger, median of `confirm` rounds each
                 ta, tb = [], []
