@@ -169,9 +169,12 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 // V^T [64][328]: both row strides keep the 8/16-byte fragment reads conflict-free), one
 // barrier, then every wave runs the same online-softmax loop over 64-key tiles.
 constexpr int AW_TK = 256;
-constexpr int AW_VROW = 328;   // V^T row stride: 164 dwords == 36 (mod 64), like AT_ROW
+constexpr int AW_VROW = 264;   // V^T row stride: 132 dwords == 4 (mod 64): the 16 dim rows of a half-wave's
+                               // 8-byte reads land 4 banks apart (q adds 2) -> conflict-free
 
-__global__ __launch_bounds__(1024) void attn_head_kernel(AttnArgs a) {
+// capped at 64 VGPRs (8 waves per SIMD, no spill) with a 70.7 KB LDS map so two 13-wave heads can
+// share a CU: batch-32 ViT-B/16 attention 20.8 -> 19.0 us (profiles/attention_r3.txt)
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void attn_head_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint16_t hsm[];
   uint16_t* ks = hsm;                      // [AW_TK][AT_ROW]
   uint16_t* vt = hsm + AW_TK * AT_ROW;     // [AT_DH][AW_VROW]

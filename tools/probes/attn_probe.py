@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 from kdl.ops import _lib  # noqa: E402
 
-B, T, H, dh = 32, 197, 12, 64
+B, T, H, dh = int(os.environ.get('AP_B', 32)), 197, 12, 64
 qkv = torch.randn(B * T, 3 * H * dh, device="cuda").to(torch.bfloat16)
 out = torch.zeros(B * T, H * dh, dtype=torch.bfloat16, device="cuda")
 C = _lib.lib()
