@@ -142,6 +142,7 @@ def main(argv=None) -> int:
     ap.add_argument("--out", required=True)
     ap.add_argument("--cfgs", default=None, help="comma list: only these configs challenge the table")
     ap.add_argument("--verbose", action="store_true", help="log every challenger's graph time")
+    ap.add_argument("--margin", type=float, default=0.002, help="relative win a challenger must show (screen and A/B)")
     ap.add_argument("--tie", default=None, help=r"regex, e.g. 'encoder_layer_\d+': tune matching layers together")
     a = ap.parse_args(argv)
     from . import registry
@@ -173,7 +174,7 @@ def main(argv=None) -> int:
     t0 = time.time()
     only = {int(c) for c in a.cfgs.split(",")} if a.cfgs else None
     table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only,
-                       tie=a.tie, verbose=a.verbose)
+                       tie=a.tie, verbose=a.verbose, margin=a.margin)
     Path(a.out).write_text(json.dumps(table, indent=1))
     print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
     return 0
