@@ -157,7 +157,7 @@ BlasLtArgs blaslt_args(const py::dict& d) {
   a.res = P<const void>(d, "res"); a.bias = P<const float>(d, "bias");
   a.M = I(d, "M"); a.N = I(d, "N"); a.K = I(d, "K");
   a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
-  a.relu = I(d, "relu"); a.dt = I(d, "dt"); a.algo = I(d, "algo");
+  a.act = I(d, "act"); a.dt = I(d, "dt"); a.algo = I(d, "algo");
   a.wscale = P<const float>(d, "wscale");
   return a;
 }

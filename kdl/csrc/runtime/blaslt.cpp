@@ -69,9 +69,11 @@ int blaslt_prepare(BlasLtArgs& a) {
   const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   ck(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)), "transA");
   ck(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)), "transB");
-  hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_DEFAULT;
-  if (a.bias) epi = a.relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS;
-  else if (a.relu) epi = HIPBLASLT_EPILOGUE_RELU;
+  if (a.act < 0 || a.act > 2) throw std::invalid_argument("blaslt: act is 0 (none), 1 (ReLU) or 2 (GELU)");
+  static const hipblasLtEpilogue_t kEpi[2][3] = {
+      {HIPBLASLT_EPILOGUE_DEFAULT, HIPBLASLT_EPILOGUE_RELU, HIPBLASLT_EPILOGUE_GELU},
+      {HIPBLASLT_EPILOGUE_BIAS, HIPBLASLT_EPILOGUE_RELU_BIAS, HIPBLASLT_EPILOGUE_GELU_BIAS}};
+  hipblasLtEpilogue_t epi = kEpi[a.bias ? 1 : 0][a.act];
   ck(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)), "epilogue");
   if (a.bias) {
     const void* bp = a.bias;

@@ -26,7 +26,7 @@ struct BlasLtArgs {
   const void* res = nullptr;    // [M][ldr] residual (C operand, beta = 1) or null
   const float* bias = nullptr;  // [N] fp32 or null
   int M = 0, N = 0, K = 0, ldx = 0, ldy = 0, ldr = 0;
-  int relu = 0;                 // 1: ReLU applied last, after bias and the residual C
+  int act = 0;                  // applied last, after bias and the residual C: 1 ReLU, 2 GELU (hipBLASLt's)
   int dt = 0;                   // 0 bf16, 1 fp16 (x, w, y, res); 2: x, w OCP e4m3, y / res bf16
   const float* wscale = nullptr;  // dt 2: per-output-channel [N] dequant scale of w (x scale folded in)
   int algo = 0;                 // rank in the heuristic list (clamped to the list's length)

@@ -66,8 +66,9 @@ class ViTEngine(EngineBase):
     def _lin(self, name: str, w: torch.Tensor, b: torch.Tensor, relu_out: int = 0,
              blaslt: bool = True) -> ConvGemmLayer:
         # blaslt: hipBLASLt is a tuning candidate for the plain linears (bias, or bias + the
-        # residual as its C operand); not for mlp.0 (exact-erf GELU epilogue) or the patch
-        # embedding (writes into per-image token rows)
+        # residual as its C operand); not for mlp.0 (hipBLASLt's GELU epilogue measured 64.2 vs
+        # 58.4 us for our exact-erf one, profiles/vit_blaslt_r3.txt) or the patch embedding
+        # (writes into per-image token rows)
         lay = ConvGemmLayer(name, MODE_PW, w.double(), b.float(), cin_pad=w.shape[1], n=w.shape[0],
                             relu_out=relu_out, device=self.device, blaslt=blaslt and relu_out != 3)
         lay.krot = 1    # K-rotated LDS-DMA GEMM: bf16 +0.6 % img/s, p50 -2.9 % (profiles/krot_ab.txt)

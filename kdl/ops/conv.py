@@ -229,8 +229,8 @@ class ConvGemmLayer:
         self.w_ref = w_nk.to(dtype).float()
         self.w_plain = None
         if blaslt:
-            assert mode == MODE_PW and stride == 1 and self.relu_out in (0, 1, 2) and not relu_in, \
-                (name, "hipBLASLt node: plain linear, bias / ReLU / residual epilogues only")
+            assert mode == MODE_PW and stride == 1 and self.relu_out in (0, 1, 2, 3) and not relu_in, \
+                (name, "hipBLASLt node: plain linear, bias / ReLU / GELU / residual epilogues only")
             self.w_plain = w_nk.to(dtype).to(device).contiguous()
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
         # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
@@ -296,12 +296,15 @@ class ConvGemmLayer:
 
     def blaslt_args(self, x: int, y: int, M: int, res: int | None = None, ldx: int | None = None,
                     ldr: int | None = None, algo: int = 0) -> dict:
-        # relu_out 1 is ReLU BEFORE the residual add, which hipBLASLt (act after C) cannot express
+        # relu_out 1 is ReLU BEFORE the residual add, which hipBLASLt (act after C) cannot express;
+        # relu_out 3 (GELU) maps to hipBLASLt's GELU epilogue (profiles/vit_blaslt_r3.txt: its form
+        # vs the exact-erf GELU of our kernels), no residual
         assert self.w_plain is not None, (self.name, "layer built without blaslt=True")
-        assert not (res and self.relu_out == 1), (self.name, "ReLU before the residual add")
+        assert not (res and self.relu_out in (1, 3)), (self.name, "activation before the residual add")
         return dict(x=x, w=_lib.ptr(self.w_plain), y=y, res=res, bias=_lib.ptr(self.bias), M=M, N=self.n,
                     K=self.K, ldx=ldx if ldx is not None else self.cin_pad, ldy=self.ldy,
-                    ldr=ldr if ldr is not None else self.ldy, relu=int(self.relu_out != 0), dt=self.dt, algo=algo)
+                    ldr=ldr if ldr is not None else self.ldy, act={0: 0, 1: 1, 2: 1, 3: 2}[self.relu_out],
+                    dt=self.dt, algo=algo)
 
     def _emit_blaslt(self, prog, x, y, g: Geometry, res, ldx, ldr, cfg: int, opad: int) -> None:
         assert opad == 0 and g.H == g.OH and g.W == g.OW, (self.name, "hipBLASLt node: dense rows only")

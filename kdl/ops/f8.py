@@ -96,7 +96,7 @@ class F8Linear:
         if is_blaslt(cfg):
             assert self.w8_plain is not None and a["y"] and not a["y8"], (self.name, "hipBLASLt: bf16 output only")
             d = dict(x=a["x"], w=_lib.ptr(self.w8_plain), y=a["y"], res=a["res"], bias=a["bias"], M=a["M"],
-                     N=self.n, K=self.k, ldx=self.k, ldy=a["ldy"], ldr=a["ldr"], relu=0, dt=2,
+                     N=self.n, K=self.k, ldx=self.k, ldy=a["ldy"], ldr=a["ldr"], act=0, dt=2,
                      wscale=a["colscale"], algo=cfg - BLT_BASE)
             if prog is None:
                 _lib.lib().blaslt(d, _lib.stream_ptr())

@@ -24,11 +24,13 @@ def test_blaslt_ids_are_offered_only_when_asked():
 def test_blaslt_epilogue_mapping():
     x, y, r = 0x1000, 0x2000, 0x3000
     d = _lin(relu_out=0).blaslt_args(x, y, M=100, res=r, algo=3)
-    assert (d["relu"], d["res"], d["algo"], d["N"], d["K"], d["ldy"]) == (0, r, 3, 128, 64, 128)
-    assert _lin(relu_out=2).blaslt_args(x, y, M=100, res=r)["relu"] == 1   # ReLU after the residual: C then act
-    assert _lin(relu_out=1).blaslt_args(x, y, M=100)["relu"] == 1          # ReLU without a residual
-    with pytest.raises(AssertionError):                                   # ReLU BEFORE the add: not expressible
-        _lin(relu_out=1).blaslt_args(x, y, M=100, res=r)
+    assert (d["act"], d["res"], d["algo"], d["N"], d["K"], d["ldy"]) == (0, r, 3, 128, 64, 128)
+    assert _lin(relu_out=2).blaslt_args(x, y, M=100, res=r)["act"] == 1    # ReLU after the residual: C then act
+    assert _lin(relu_out=1).blaslt_args(x, y, M=100)["act"] == 1           # ReLU without a residual
+    assert _lin(relu_out=3).blaslt_args(x, y, M=100)["act"] == 2           # GELU
+    for ro in (1, 3):                                                      # activation BEFORE the add
+        with pytest.raises(AssertionError):
+            _lin(relu_out=ro).blaslt_args(x, y, M=100, res=r)
 
 
 def test_blaslt_refused_for_fused_lowerings():
@@ -36,8 +38,6 @@ def test_blaslt_refused_for_fused_lowerings():
     w, b = torch.randn(64, 32, generator=g, dtype=torch.float64), torch.randn(64, generator=g)
     with pytest.raises(AssertionError):
         ConvGemmLayer("sep", MODE_DW, w, b, cin_pad=32, n=64, dww=torch.randn(9, 32), device="cpu", blaslt=True)
-    with pytest.raises(AssertionError):
-        ConvGemmLayer("gelu", MODE_PW, w, b, cin_pad=32, n=64, relu_out=3, device="cpu", blaslt=True)
     with pytest.raises(AssertionError):
         ConvGemmLayer("s2", MODE_PW, w, b, cin_pad=32, n=64, stride=2, device="cpu", blaslt=True)
 

@@ -29,6 +29,7 @@ def _layer(N, K, relu_out=0, dtype=torch.bfloat16, seed=0):
     (197, 768, 768, 0, True, torch.bfloat16),       # one image of out_proj
     (1000, 256, 64, 1, False, torch.float16),       # ResNet conv1-like: bias + ReLU
     (1000, 256, 64, 2, True, torch.float16),        # ResNet conv3-like: ReLU after the residual add
+    (6304, 3072, 768, 3, False, torch.bfloat16),    # ViT mlp.0: bias + GELU (hipBLASLt's form)
 ])
 def test_blaslt_linear_matches_fp32(M, N, K, relu_out, res, dtype):
     lay = _layer(N, K, relu_out, dtype)
@@ -38,7 +39,9 @@ def test_blaslt_linear_matches_fp32(M, N, K, relu_out, res, dtype):
     ref = x.float() @ lay.w_ref.to(DEV).T + lay.bias[:N].float()
     if res:
         ref = ref + r[:, :N].float()
-    if relu_out:
+    if relu_out == 3:
+        ref = torch.nn.functional.gelu(ref)
+    elif relu_out:
         ref = ref.clamp_min(0)
     geo = Geometry(1, 1, M, 1, M)
     for algo in range(BLT_ALGOS):
@@ -102,4 +105,5 @@ def test_blaslt_e4m3_linear_matches_dequantized_reference():
         lay.emit(None, cfg=BLT_BASE + algo, x8=x8.data_ptr(), M=M, y=y.data_ptr(), res=y.data_ptr(), ldy=N)
         torch.cuda.synchronize()
         assert _rel(y, ref) < 1e-2, algo
+
 
