@@ -46,6 +46,9 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.pH = I(d, "pH"); a.pW = I(d, "pW"); a.pld = I(d, "pld"); a.ppad = I(d, "ppad");
   a.wimg = I(d, "wimg");
   a.krot = I(d, "krot");
+  a.ksplit = I(d, "ksplit");
+  a.ws = P<float>(d, "ws");
+  a.cnt = P<int>(d, "cnt");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {

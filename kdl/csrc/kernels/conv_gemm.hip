@@ -291,7 +291,8 @@ static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (a.K % 32 != 0 || a.M <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
-  // per-image weights: the LDS-DMA pipelined GEMM only
+  // split-K and per-image weights: the LDS-DMA pipelined GEMM only
+  if (a.ksplit > 1 && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE)) return hipErrorInvalidValue;
   if (a.wimg && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE || a.wimg < 0)) return hipErrorInvalidValue;
   if (a.dt == 1) {   // fp16: the pointwise / implicit-3x3 GEMMs only
     if (cfg >= SEP_CFG_BASE) return hipErrorInvalidValue;

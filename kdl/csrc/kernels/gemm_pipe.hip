@@ -55,8 +55,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   // per-image weights (a.wimg): M tiles are cut per image so a tile has one weight set
   const int mpi = a.wimg ? (OHW + BM - 1) / BM : 0;
   const int nM = a.wimg ? a.B * mpi : (a.M + BM - 1) / BM;
-  const int wg = xcd_remap(blockIdx.x, nM * nN);
-  const int mi = wg / nN, ni = wg % nN;
+  // split-K: consecutive logical ids are the splits of one tile (same XCD: their partials meet in L2)
+  const int S = a.ksplit > 1 ? a.ksplit : 1;
+  const int tiles = nM * nN;
+  const int wid = xcd_remap(blockIdx.x, tiles * S);
+  const int ksid = wid % S, tile = wid / S;
+  const int mi = tile / nN, ni = tile % nN;
   int m0 = mi * BM, mend = a.M;
   long wofs = 0;
   if (a.wimg) {
@@ -66,7 +70,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     wofs = (long)bi * a.wimg;
   }
   const int n0 = ni * BN;
-  const int KT32 = a.K >> 5;                  // 32-deep k steps
+  const int KT32 = (a.K >> 5) / S;           // 32-deep k steps of this split (host: divisible)
+  const int kb = ksid * KT32;                 // its first k step
   const int KT = (KT32 + KSUB - 1) / KSUB;    // pipeline stages
 
   // per-lane source offsets of the fragments this wave stages
@@ -83,21 +88,21 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       src[i] = pix * a.ldx + 8 * (lane >> 4);
     } else {
       const int nf = n0 / 16 + (f - AF);
-      src[i] = wofs + ((long)nf * KT32) * 512 + lane * 8;
+      src[i] = wofs + ((long)nf * (a.K >> 5)) * 512 + lane * 8;
     }
   }
 
   // Issue stage t (k32 steps t*KSUB .. t*KSUB+KSUB-1). A sub-step past the end
   // of K re-issues the stage's first sub-step into its own slot (its MFMAs are
   // skipped), so every stage has exactly L*KSUB DMAs for the counted vmcnt.
-  const int krot = a.krot ? (mi * 7) % KT32 : 0;
+  const int krot = a.krot && S == 1 ? (mi * 7) % KT32 : 0;
   auto issue = [&](int t, int buf) {
 #pragma unroll
     for (int ks = 0; ks < KSUB; ++ks) {
       int k32 = t * KSUB + ks;
       if (k32 >= KT32) k32 = t * KSUB;
       k32 += krot;                            // uniform: rotated k order (0 = in order)
-      k32 = k32 >= KT32 ? k32 - KT32 : k32;
+      k32 = (k32 >= KT32 ? k32 - KT32 : k32) + kb;
       long koff_a;
       if constexpr (MODE == 0) {
         koff_a = (long)k32 * 32;
@@ -154,6 +159,48 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     }
   }
   wait_vm_barrier<0>();
+
+  if (S > 1) {
+    // fp32 partial of this split, fragment-linear (each wave writes 1 KiB per fragment)
+    float4* const part = (float4*)a.ws + (long)tile * (BM * BN / 4);
+    const long sstride = (long)tiles * (BM * BN / 4);
+    auto pidx = [&](int i, int j) { return ((wave * FM + i) * FN + j) * 64 + lane; };
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        part[ksid * sstride + pidx(i, j)] = (float4){acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+    // publish (every storing wave drains, barrier, agent release, count) and elect the last split
+    // the election flag lives in the (idle) pipeline LDS: a second __shared__ object can make hipcc
+    // wait vmcnt(0) before every k-step's first LDS read (cdna_hip_programming.md §5 trap (a))
+    int& s_last = *(int*)smem;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == S - 1;
+      if (s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const bool last = s_last;
+    __syncthreads();                          // every thread read the flag before the C tile reuses the LDS
+    if (!last) return;                        // uniform: the whole workgroup leaves
+    for (int sp = 0; sp < S; ++sp) {
+      if (sp == ksid) continue;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const float4 v = part[sp * sstride + pidx(i, j)];
+          acc[i][j][0] += v.x; acc[i][j][1] += v.y; acc[i][j][2] += v.z; acc[i][j][3] += v.w;
+        }
+    }
+  }
 
   // epilogue: bias + ReLU -> bf16 C tile in LDS -> (+residual) 16-byte stores
   const int quad = lane >> 4, col = lane & 15;
@@ -224,7 +271,9 @@ static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
   if (a.wimg && (a.M != a.B * a.OH * a.OW || a.B <= 0)) return hipErrorInvalidValue;
   const int nM = a.wimg ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT>), dim3(nM * nN),
+  const int S = a.ksplit > 1 ? a.ksplit : 1;
+  if (S > 1 && ((a.K / 32) % S != 0 || !a.ws || !a.cnt || a.wimg || S > 16)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT>), dim3(nM * nN * S),
                      dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();
 }

@@ -47,6 +47,14 @@ struct ConvGemmArgs {
   // step ((7*mi) mod K/32), so the workgroups sharing the weights do not all fetch the same
   // fragments at launch (env KDL_PIPE_KROT overrides; 0 = in order)
   int krot;
+  // split-K (gemm_pipe only; ResNet-50's layer3/4 3x3 convs: M = 6272 / 1568 rows fill a quarter to a
+  // half of the 256 CUs with whole-K tiles): ksplit > 1 workgroups per output tile each reduce K/ksplit
+  // k-steps into fp32 partials at ws ([ksplit][tiles][BM*BN], fragment-linear); the last of a tile to
+  // arrive (per-tile counter cnt, agent-scope release/acquire, reset to 0 by that workgroup) sums
+  // them and runs the normal epilogue. K/32 must divide by ksplit.
+  int ksplit;
+  float* ws;
+  int* cnt;
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);

@@ -17,7 +17,7 @@ from pathlib import Path
 import torch
 
 from ..ops import _lib
-from ..ops.conv import MODE_DW, ConvGemmLayer, is_blaslt
+from ..ops.conv import MODE_DW, ConvGemmLayer, is_blaslt, is_splitk, splitk_parts
 
 
 @dataclass
@@ -255,6 +255,9 @@ class EngineBase:
             split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
             ok = cfg in s.layer.candidates or (is_blaslt(cfg) and (getattr(s.layer, "w_plain", None) is not None
                                                                    or getattr(s.layer, "w8_plain", None) is not None))
+            if is_splitk(cfg):
+                sk, base = splitk_parts(cfg)
+                ok = sk in getattr(s.layer, "ksplit", ()) and base in s.layer.candidates
             if ok and (not split or getattr(s.layer, "mode", -1) == MODE_DW):
                 s.layer.split, s.layer.cfg = split, cfg
         self.invalidate()

@@ -92,12 +92,15 @@ class ResNetEngine(EngineBase):
             self.shapes[tpad] = (H, H, wdt, 1)
             self.shapes[tmid] = (oh, oh, wdt, 0)
             w1, b1 = _fold(p, f"{blk.prefix}.conv1.weight", f"{blk.prefix}.bn1")
+            # split-K candidates where the output map is 14x14 or 7x7 (layer3 / layer4): M = 32 x 196 /
+            # 32 x 49 rows fill only a fraction of the 256 CUs with whole-K tiles
+            sk = (2, 3, 4) if oh <= 14 else ()
             l1 = ConvGemmLayer(f"{blk.prefix}.conv1", MODE_PW, w1, b1, cin_pad=blk.cin, n=wdt,
-                               relu_out=1, device=dev, dtype=self.dtype)
+                               relu_out=1, device=dev, dtype=self.dtype, ksplit=sk if H <= 14 else ())
             self.steps.append(Step("conv", l1.name, l1, cur, tpad, geom=(H, H, H, H), extra=dict(opad=1)))
             w2, b2 = _fold(p, f"{blk.prefix}.conv2.weight", f"{blk.prefix}.bn2")
             l2 = ConvGemmLayer(f"{blk.prefix}.conv2", MODE_CONV, w2, b2, cin_pad=wdt, n=wdt,
-                               stride=blk.stride, relu_out=1, device=dev, dtype=self.dtype)
+                               stride=blk.stride, relu_out=1, device=dev, dtype=self.dtype, ksplit=sk)
             self.steps.append(Step("conv", l2.name, l2, tpad, tmid, geom=(H + 2, H + 2, oh, oh)))
             if blk.downsample:
                 sc = f"sc{oh}_{cout}"
@@ -114,7 +117,7 @@ class ResNetEngine(EngineBase):
             self.shapes[out] = (oh, oh, cout, 0)
             w3, b3 = _fold(p, f"{blk.prefix}.conv3.weight", f"{blk.prefix}.bn3")
             l3 = ConvGemmLayer(f"{blk.prefix}.conv3", MODE_PW, w3, b3, cin_pad=wdt, n=cout, relu_out=2,
-                               device=dev, dtype=self.dtype)
+                               device=dev, dtype=self.dtype, ksplit=sk)
             self.steps.append(Step("conv", l3.name, l3, tmid, out, res=res, geom=(oh, oh, oh, oh)))
             cur, H = out, oh
         nf = (self.classes + 15) // 16

@@ -81,6 +81,9 @@ SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
 # layers built with blaslt=True; id - BLT_BASE = rank in hipBLASLt's heuristic list for the shape
 BLT_BASE = 1000
 BLT_ALGOS = 6
+# ids >= SPLITK_BASE: an LDS-DMA GEMM config (16..63) with K split over ksplit workgroups per tile
+# (gemm_pipe.hip ConvGemmArgs.ksplit): SPLITK_BASE + 100 * ksplit + base id
+SPLITK_BASE = 2000
 # ws configs with a chained (multi-layer, one launch) variant: sepconv_ws.hip KDL_CHAIN_CONFIGS
 CHAIN_CONFIGS = (143, 144, 146)
 # never autotune candidates: the ws stamping build and band ablation, the pooled sepconv (seppool only)
@@ -134,12 +137,28 @@ def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | No
 
 
 def is_blaslt(cfg: int) -> bool:
-    return cfg >= BLT_BASE
+    return BLT_BASE <= cfg < SPLITK_BASE
+
+
+def is_splitk(cfg: int) -> bool:
+    return cfg >= SPLITK_BASE
+
+
+def splitk_parts(cfg: int) -> tuple[int, int]:
+    """split-K id -> (ksplit, base LDS-DMA GEMM config)."""
+    return (cfg - SPLITK_BASE) // 100, (cfg - SPLITK_BASE) % 100
+
+
+def splitk_id(ksplit: int, base: int) -> int:
+    assert 2 <= ksplit <= 16 and PIPE_BASE <= base < SEP_BASE, (ksplit, base)
+    return SPLITK_BASE + 100 * ksplit + base
 
 
 def cfg_tile(cfg: int) -> tuple[int, int]:
     if is_blaslt(cfg):          # no tile of ours: channels are stored unpadded (16-granular)
         return 256, 16
+    if is_splitk(cfg):
+        cfg = splitk_parts(cfg)[1]
     fm, fn, wgm, wgn = CONFIGS[cfg]
     return 16 * fm * wgm, 16 * fn * wgn
 
@@ -193,9 +212,11 @@ class ConvGemmLayer:
                  cin_pad: int, n: int, stride: int = 1, dww: torch.Tensor | None = None,
                  relu_in: bool = False, relu_out: bool | int = False, device="cuda",
                  candidates: list[int] | None = None, dtype: torch.dtype = torch.bfloat16,
-                 blaslt: bool = False):
+                 blaslt: bool = False, ksplit: tuple = ()):
         """``dtype``: element type of the activations and packed weights, bf16 (default)
         or fp16 (MODE_PW / MODE_CONV only; ``dt`` = 1 in the launch args).
+        ``ksplit``: split-K factors to offer with the LDS-DMA GEMM tiles of at most 128 rows
+        (ids >= SPLITK_BASE; for layers whose M fills few CUs: ResNet-50 layer3/4).
         ``blaslt``: also offer the hipBLASLt GEMM node (ids >= BLT_BASE) as a variant; only
         for a plain stride-1 pointwise linear whose epilogue is bias (+ReLU) (+residual
         as hipBLASLt's C operand, ReLU last) -- keeps an unpacked [N][K] weight copy."""
@@ -227,6 +248,9 @@ class ConvGemmLayer:
             self.dwk = pack_dw_entries(dww).to(device)
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
         self.w_ref = w_nk.to(dtype).float()
+        self.ksplit = tuple(ksplit)
+        assert not self.ksplit or mode in (MODE_PW, MODE_CONV), (name, "split-K: LDS-DMA GEMM lowerings only")
+        self._splitk_bufs: tuple | None = None     # (fp32 partials, per-tile counters), grown on demand
         self.w_plain = None
         if blaslt:
             assert mode == MODE_PW and stride == 1 and self.relu_out in (0, 1, 2, 3) and not relu_in, \
@@ -239,12 +263,14 @@ class ConvGemmLayer:
     def variants(self, W: int | None = None) -> list[tuple[bool, int]]:
         """(split, cfg) pairs valid for this layer (``W``: image width, filters the
         fused separable configs whose LDS row band would not fit)."""
+        skv = [(False, splitk_id(sk, c)) for sk in self.ksplit for c in self.candidates
+               if PIPE_BASE <= c < SEP_BASE and cfg_tile(c)[0] <= 128 and (self.K // 32) % sk == 0]
         if self.mode == MODE_CONV:
             return [(False, c) for c in self.candidates
-                    if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))]
+                    if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))] + skv
         if self.mode != MODE_DW:
             blt = [(False, BLT_BASE + i) for i in range(BLT_ALGOS)] if self.w_plain is not None else []
-            return [(False, c) for c in self.candidates if c < SEP_BASE] + blt
+            return [(False, c) for c in self.candidates if c < SEP_BASE] + blt + skv
         return ([(False, c) for c in self.candidates
                  if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W, self.K, self.n)]
                 + [(True, c) for c in self.candidates if c < SEP_BASE])
@@ -283,6 +309,17 @@ class ConvGemmLayer:
                 prog.add_dw(self.name + "/dw", da)
                 prog.add_conv_gemm(self.name, MODE_PW, cfg, ga)
             return
+        if is_splitk(cfg):
+            sk, cfg = splitk_parts(cfg)
+            assert pool is None and wimg is None and (self.K // 32) % sk == 0, (self.name, sk)
+            ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
+            ws, cnt = self._splitk_workspace(sk, cfg, g.M)
+            ga.update(ksplit=sk, ws=_lib.ptr(ws), cnt=_lib.ptr(cnt))
+            if prog is None:
+                C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
+            else:
+                prog.add_conv_gemm(self.name, self.mode, cfg, ga)
+            return
         ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
         if pool:
             ga.update(pool)
@@ -313,6 +350,23 @@ class ConvGemmLayer:
             _lib.lib().blaslt(d, _lib.stream_ptr())
         else:
             prog.add_blaslt(self.name, d)
+
+    def _splitk_workspace(self, ksplit: int, cfg: int, M: int):
+        """fp32 partials [ksplit][tiles][BM*BN] and zeroed per-tile counters (the last split of a tile
+        resets its counter, so graph replays need no memset). One pair per layer, grown to the largest
+        request: a layer's launches never overlap (one stream per engine / pipeline stage)."""
+        bm, bn = cfg_tile(cfg)
+        tiles = -(-M // bm) * (self.nf(cfg) * 16 // bn)
+        need_ws, need_cnt = ksplit * tiles * bm * bn, tiles
+        cur = self._splitk_bufs
+        if cur is None or cur[0].numel() < need_ws or cur[1].numel() < need_cnt:
+            dev = self.wp.device
+            n_ws = max(need_ws, cur[0].numel() if cur else 0)
+            n_cnt = max(need_cnt, cur[1].numel() if cur else 0)
+            self._splitk_bufs = (torch.zeros(n_ws, dtype=torch.float32, device=dev),
+                                 torch.zeros(n_cnt, dtype=torch.int32, device=dev))
+            self._splitk_old = getattr(self, "_splitk_old", []) + ([cur] if cur else [])   # captured graphs may hold them
+        return self._splitk_bufs
 
     def nf(self, cfg: int | None = None) -> int:
         cfg = self.cfg if cfg is None else cfg

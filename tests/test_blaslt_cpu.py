@@ -54,3 +54,17 @@ def test_tuning_table_selects_blaslt_only_where_built():
     assert eng.steps[0].layer.cfg == BLT_BASE + 2
     assert not is_blaslt(eng.steps[1].layer.cfg)          # refused: no unpacked weights on that layer
     assert eng.tuning()["l0"] == [0, BLT_BASE + 2]
+
+
+def test_splitk_ids_variants_and_tuning():
+    from kdl.ops.conv import MODE_CONV, is_splitk, splitk_id, splitk_parts
+    g = torch.Generator().manual_seed(2)
+    lay = ConvGemmLayer("c2", MODE_CONV, torch.randn(256, 9 * 256, generator=g, dtype=torch.float64),
+                        torch.randn(256, generator=g), cin_pad=256, n=256, device="cpu", ksplit=(2, 3))
+    sk = [c for _, c in lay.variants(14) if is_splitk(c)]
+    assert sk and all(splitk_parts(c)[0] in (2, 3) and cfg_tile(c)[0] <= 128 for c in sk)
+    assert splitk_parts(splitk_id(3, 16)) == (3, 16) and not is_blaslt(splitk_id(3, 16))
+    plain = _lin()                                             # built without ksplit: refused
+    eng = _Eng([lay, plain])
+    eng.apply_tuning({"l0": [0, sk[0]], "l1": [0, splitk_id(2, 16)]})
+    assert eng.steps[0].layer.cfg == sk[0] and not is_splitk(eng.steps[1].layer.cfg)
