@@ -164,10 +164,12 @@ static void pool_rows_plan(const PoolAddArgs& a, int* seg, int* rb, int* nseg, i
   *nb = (a.OH + R - 1) / R;
 }
 
+// default: the row-streaming kernel (Xception bench +0.5-1.0 % in three A/B pairs, profiles/pool_algo_ab_r3.txt);
+// KDL_POOL_ALGO=1 restores the pixel-per-thread kernel
 static int pool_algo(const PoolAddArgs& a) {
   if (a.algo > 0) return a.algo;
   static const int env = [] { const char* e = getenv("KDL_POOL_ALGO"); return e ? atoi(e) : 0; }();
-  return env > 0 ? env : 1;
+  return env > 0 ? env : 2;
 }
 
 hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {

@@ -183,7 +183,8 @@ class ResNetEngine(EngineBase):
         elif step.kind == "pool":
             prog.add_pool_add(step.name, dict(x=self._ptr(step.src), res=None, y=self._ptr(step.dst),
                                               B=b, H=H, W=W, OH=OH, OW=OW, C=step.extra["C"],
-                                              pad_top=1, pad_left=1, dt=self.dt))
+                                              pad_top=1, pad_left=1, dt=self.dt,
+                                              algo=1))   # pixel-per-thread: row-streaming measured -0.3 %
         elif step.kind == "conv":
             self._emit_conv(prog, step, b)
         elif step.kind == "gap":
