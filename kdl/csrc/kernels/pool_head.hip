@@ -196,107 +196,79 @@ hipError_t pool_add(const PoolAddArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Classifier head as three small kernels. The head is bound by PER-CU bandwidth,
-// not by the chip: the previous one-block-per-image kernel put the whole 800 KB
-// Dense1 matrix through each of only 32 CUs (35-39 us at batch 32). Here
-//   gap_kernel    grid (B, F/256): 8 pixel groups x 32 channel chunks per block,
-//                 partial sums reduced through LDS -> feat [B][F] fp32;
-//   dense1_kernel grid F/64: K-split, w1 TRANSPOSED to [H1][F] at load time and read
-//                 once chip-wide -> partials [F/64][B][H1];
-//   dense2_kernel one block per image: partials (+b1, ReLU) and w2 in LDS, 16 lanes per logit.
+// Classifier head as two small kernels. The head is bound by PER-CU bandwidth, not by the
+// chip: a one-block-per-image kernel put the whole 800 KB Dense1 matrix through each of only
+// 32 CUs (35-39 us at batch 32). Here
+//   gap_dense1_kernel grid (F/64, B/8): GAP of 64 features x 8 images + their K-split dense1
+//                     partials [F/64][B][H1];
+//   dense2_kernel     one block per image: partials (+b1, ReLU) and w2 in LDS, 16 lanes per logit.
 // Every sum is in a fixed order: deterministic logits.
-__global__ __launch_bounds__(256) void gap_kernel(HeadArgs a) {
-  __shared__ float part[8][256];
-  const int b = blockIdx.x, c0 = blockIdx.y * 256, tid = threadIdx.x;
-  const int c8 = tid & 31, pg = tid >> 5;       // 32 chunks of 8 channels x 8 pixel groups
-  const uint16_t* xb = a.x + (long)b * a.HW * a.ldx + c0 + c8 * 8;
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (c0 + c8 * 8 < a.F) {
-#pragma unroll 16
-    for (int p = pg; p < a.HW; p += 8) {
-      const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        s[2 * d] += bf_lo(v[d]);
-        s[2 * d + 1] += bf_hi(v[d]);
-      }
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < 8; ++d) part[pg][c8 * 8 + d] = s[d];
-  __syncthreads();
-  float t = 0.f;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) t += part[g][tid];
-  if (c0 + tid < a.F) a.feat[(long)b * a.F + c0 + tid] = t * (1.0f / (float)a.HW);
-}
+constexpr int D1_K = 64;   // features per K-split block of dense1
 
-// Dense1 split over K: block kb owns features [64kb, 64kb+64) for ALL images and ALL
-// hidden units, so w1 is read exactly once chip-wide and every block's operands sit in
-// LDS (w1 slice [H1][64], features [B][64]). Thread (o, image half) keeps 16 image
-// accumulators; the feature reads are wave-wide broadcasts, the w1 reads conflict-free
-// float4s. Partial sums go to part[kb][b][o]; dense2 reduces them in a fixed order.
-constexpr int D1_K = 64;
-__global__ __launch_bounds__(256) void dense1_kernel(HeadArgs a) {
+// GAP + dense1, K-split: block (kb, image octet) averages features [64kb, 64kb+64) of 8 images
+// itself (4 pixel groups per (image, 8-channel chunk), fixed order), stages the w1 slice [H1][64]
+// (w1 TRANSPOSED to [H1][F] at load time, so each slice is read by only B/8 blocks) and writes
+// partials [F/64][B][H1]; 32 x 4 = 128 blocks at batch 32. Replaced round 2's separate GAP
+// (B x F/256 blocks) + dense1 (F/64 blocks) launches: head 22.5 -> 15.4 us, no [B][F] round trip.
+__global__ __launch_bounds__(256) void gap_dense1_kernel(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) float w1s[128][D1_K + 4];
-  __shared__ __attribute__((aligned(16))) float fs[64][D1_K];
+  __shared__ __attribute__((aligned(16))) float gp[4][8][D1_K];   // pixel-group partial sums
+  __shared__ __attribute__((aligned(16))) float fs[8][D1_K];
   const int kb = blockIdx.x, k0 = kb * D1_K, tid = threadIdx.x;
-  const int bb = blockIdx.y * 64;               // image block of this workgroup
-  const int bmax = min(a.B - bb, 64);
-  // staging: fixed trip counts, fully unrolled, so every load of a thread is in flight
-  // before its first LDS store (a strided loop paid one memory latency per iteration)
+  const int ib0 = blockIdx.y * 8, nimg = min(8, a.B - ib0);
   {
-    float4 wv[8], fv[4];
+    float4 wv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + 256 * j, o = i / (D1_K / 4), c = i - o * (D1_K / 4);
       wv[j] = o < a.H1 ? *(const float4*)(a.w1 + (long)o * a.F + k0 + c * 4) : (float4){0.f, 0.f, 0.f, 0.f};
     }
+    const int item = tid & 63, img = item >> 3, c8 = item & 7, pg = tid >> 6;
+    float sm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (img < nimg) {
+      const uint16_t* xb = a.x + (long)(ib0 + img) * a.HW * a.ldx + k0 + c8 * 8;
+#pragma unroll 5
+      for (int p = pg; p < a.HW; p += 4) {
+        const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + 256 * j, b = i / (D1_K / 4), c = i - b * (D1_K / 4);
-      fv[j] = b < bmax ? *(const float4*)(a.feat + (long)(bb + b) * a.F + k0 + c * 4) : (float4){0.f, 0.f, 0.f, 0.f};
+        for (int d = 0; d < 4; ++d) {
+          sm[2 * d] += bf_lo(v[d]);
+          sm[2 * d + 1] += bf_hi(v[d]);
+        }
+      }
     }
+#pragma unroll
+    for (int d = 0; d < 8; ++d) gp[pg][img][c8 * 8 + d] = sm[d];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + 256 * j, o = i / (D1_K / 4), c = i - o * (D1_K / 4);
       *(float4*)&w1s[o][c * 4] = wv[j];
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + 256 * j, b = i / (D1_K / 4), c = i - b * (D1_K / 4);
-      *(float4*)&fs[b][c * 4] = fv[j];
-    }
   }
   __syncthreads();
-  // thread = 4 hidden units x 8 images: 12 LDS float4 reads feed 128 FMAs per k-quad
-  // (a thread per unit streaming every image was LDS-issue bound: 1 read per 4 FMAs)
-  const int ob = tid % 32, ib = tid / 32;       // 32 unit-quads x 8 image-octets
-  const int o0 = ob * 4, i0 = ib * 8;
-  if (o0 < a.H1 && i0 < bmax) {
-    float acc[4][8];
+  const float inv = 1.0f / (float)a.HW;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[r][i] = 0.f;
-#pragma unroll 2
+  for (int r = 0; r < 2; ++r) {
+    const int i = tid + 256 * r, img = i >> 6, c = i & 63;
+    fs[img][c] = (gp[0][img][c] + gp[1][img][c] + gp[2][img][c] + gp[3][img][c]) * inv;
+  }
+  __syncthreads();
+  // thread = hidden unit o x 4 images
+  const int o = tid & 127, i0 = (tid >> 7) * 4;
+  if (o < a.H1) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
     for (int k = 0; k < D1_K; k += 4) {
-      float4 w[4], f[8];
+      const float4 w = *(const float4*)&w1s[o][k];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) w[r] = *(const float4*)&w1s[min(o0 + r, 127)][k];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) f[i] = *(const float4*)&fs[min(i0 + i, 63)][k];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          acc[r][i] += w[r].x * f[i].x + w[r].y * f[i].y + w[r].z * f[i].z + w[r].w * f[i].w;
+      for (int i = 0; i < 4; ++i) {
+        const float4 f = *(const float4*)&fs[i0 + i][k];
+        acc[i] += w.x * f.x + w.y * f.y + w.z * f.z + w.w * f.w;
+      }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (o0 + r < a.H1 && i0 + i < bmax) a.hid[((long)kb * a.B + bb + i0 + i) * a.H1 + o0 + r] = acc[r][i];
+    for (int i = 0; i < 4; ++i)
+      if (i0 + i < nimg) a.hid[((long)kb * a.B + ib0 + i0 + i) * a.H1 + o] = acc[i];
   }
 }
 
@@ -339,10 +311,9 @@ __global__ __launch_bounds__(256) void dense2_kernel(HeadArgs a) {
 
 hipError_t head_dense(const HeadArgs& a, hipStream_t s) {
   if (a.F % D1_K != 0 || a.ldx % 8 != 0 || a.B <= 0 || a.H1 <= 0 || a.H1 > 128 || a.NC <= 0 ||
-      !a.feat || !a.hid)
+      !a.hid)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gap_kernel, dim3(a.B, (a.F + 255) / 256), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(dense1_kernel, dim3(a.F / D1_K, (a.B + 63) / 64), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(gap_dense1_kernel, dim3(a.F / D1_K, (a.B + 7) / 8), dim3(256), 0, s, a);
   hipLaunchKernelGGL(dense2_kernel, dim3(a.B), dim3(256), (size_t)(a.H1 + a.H1 * a.NC + 256) * sizeof(float), s, a);
   return hipGetLastError();
 }
