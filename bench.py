@@ -94,6 +94,10 @@ def main(argv=None) -> int:
     dist_on = world > 1 or a.force_dist
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # --force-dist without a launcher: a world of one (torchrun sets all of these)
+        os.environ.setdefault("MASTER_PORT", "29500")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
