@@ -2,8 +2,14 @@
 """Headline benchmark: Xception 299x299 serving throughput (images/s, whole node)
 and p50 batch latency on 1..8 MI355X (BASELINE.json metric/config).
 
-One process per GPU (``torch.distributed.run``), RCCL over xGMI. A timed step is
-one dynamic batch of 32 images per GPU (weak scaling, global batch 32*N):
+One process per GPU, RCCL over xGMI. Two equivalent entry styles:
+
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+  python bench.py --gpus N        # no launcher: bench.py spawns the N rank processes itself
+
+(the self-launch parent never touches a GPU; it refuses N > visible GPUs unless
+``--allow-shared``, which marks the JSON ``gpus_shared``). A timed step is one dynamic batch
+of 32 images per GPU (weak scaling, global batch 32*N):
 
   1. ingress (default ``--ingress local``): every rank copies its own uint8 batch
      [32,299,299,3] host(pinned)->device on a copy stream, straight into one of its
@@ -29,7 +35,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -40,9 +48,78 @@ import torch.distributed as dist
 BASELINE_IMG_S = None  # the reference publishes no throughput number
 
 
+def _visible_gpus() -> int:
+    """GPUs this process may use, counted WITHOUT touching HIP in this process: the visibility
+    env vars if set, else ``torch.cuda.device_count()`` in a throwaway child (the launcher
+    parent must stay GPU-free: it only spawns the ranks)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() != ""])
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+def _free_port() -> int:
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(a, argv: list[str]) -> int:
+    """``python bench.py --gpus N`` with no launcher: spawn the N ranks ourselves (one child
+    process per GPU, the env torch.distributed.run would set, rendezvous on 127.0.0.1) and exit
+    with the first failing child's status. Nothing here touches a GPU and nothing re-execs."""
+    n = a.gpus
+    if not a.dry_run:
+        vis = _visible_gpus()
+        if n > vis and not a.allow_shared:
+            print(f"bench.py: --gpus {n} but only {vis} GPU(s) visible; refusing to pack ranks onto "
+                  f"shared GPUs (pass --allow-shared to measure that anyway)", file=sys.stderr)
+            return 2
+    port = _free_port()
+    kids = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        kids.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    try:
+        live = list(kids)
+        while live:
+            for k in list(live):
+                c = k.poll()
+                if c is None:
+                    continue
+                live.remove(k)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for o in live:                 # one rank died: the others would hang in a collective
+                        o.terminate()
+            time.sleep(0.05)
+    finally:
+        for k in kids:
+            if k.poll() is None:
+                k.kill()
+                k.wait()
+    return rc
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of this node to use. Without a launcher (no WORLD_SIZE in the env) "
+                         "bench.py spawns the N ranks itself; under torch.distributed.run it must match "
+                         "--nproc-per-node. Default: the launcher's world size, else 1")
+    ap.add_argument("--allow-shared", action="store_true",
+                    help="permit more ranks than visible GPUs (ranks share GPUs; the JSON says gpus_shared)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launcher / rank wiring: gloo group, no GPU, one JSON line")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--settle", type=float, default=0.5,
@@ -83,12 +160,24 @@ def main(argv=None) -> int:
                          "measures the collective overhead on a 1-GPU box")
     a = ap.parse_args(argv)
 
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and a.gpus is not None and a.gpus > 1:
+        return launch_ranks(a, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    local = local % max(1, torch.cuda.device_count())
+    if a.gpus is not None and a.gpus != world:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+    if a.dry_run:
+        return dry_run(a, rank, local, world)
+    ndev = torch.cuda.device_count()
+    shared = local >= ndev
+    if shared and not a.allow_shared:
+        print(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {ndev} GPU(s) are visible; "
+              f"refusing to share a GPU (--allow-shared)", file=sys.stderr)
+        return 2
+    local = local % max(1, ndev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist_on = world > 1 or a.force_dist
@@ -324,6 +413,11 @@ def main(argv=None) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         lat = t.tolist()
 
+    gpus_shared = shared
+    if dist_on:
+        t = torch.tensor([int(shared)], device=dev, dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gpus_shared = bool(t.item())
     if rank == 0:
         ms_step = elapsed * 1e3 / a.steps
         img_s = n_global * a.steps / elapsed
@@ -353,6 +447,7 @@ def main(argv=None) -> int:
                        "per_gpu_batch": B, "parallelism": f"dp{world}",
                        "ingress": a.ingress, "egress": a.egress if dist_on else "local", "hipgraph": use_graph, "lanes": a.lanes,
                        **({"stages": f"{len(eng.ranges)} (cut after {a.stages})"} if a.stages else {})},
+            **({"gpus_shared": True} if gpus_shared else {}),
         }
         print(json.dumps(res), flush=True)
         print(f"host issue time {t_issue * 1e3 / a.steps:.3f} ms/step (ingress {tt[0] * 1e3 / a.steps:.3f}, "
@@ -362,6 +457,24 @@ def main(argv=None) -> int:
                 print(f"{name:28s} {t * 1e3:9.1f} us", file=sys.stderr)
     if dist_on:
         dist.destroy_process_group()
+    return 0
+
+
+def dry_run(a, rank: int, local: int, world: int) -> int:
+    """--dry-run: the rank wiring without a GPU (tests/test_bench_launcher.py). Every rank joins
+    a gloo group on the launcher's rendezvous, reports its env, and rank 0 prints one JSON line."""
+    print(f"bench.py dry-run rank={rank} local_rank={local} world={world} "
+          f"master={os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}", file=sys.stderr, flush=True)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.tensor([rank + 1])
+        dist.all_reduce(t)
+        assert t.item() == world * (world + 1) // 2, t
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": 0.0, "unit": "images/s", "n_gpus": world,
+                          "steps": a.steps, "warmup": a.warmup, "dry_run": True,
+                          "config": {"parallelism": f"dp{world}"}}), flush=True)
     return 0
 
 

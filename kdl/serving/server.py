@@ -104,6 +104,22 @@ def _supervise(kids: list, stop_first: list | None = None) -> int:
     return rc or next((k.returncode for k in kids if k.returncode and k.returncode > 0), 0)
 
 
+def strip_flags(argv: list[str], names: tuple[str, ...]) -> list[str]:
+    """``argv`` without the value-taking flags ``names``, in either form: ``--procs=8`` and
+    ``--procs 8`` (the child re-parses strictly, so a stray value token would kill it)."""
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        flag = a.split("=", 1)[0]
+        if flag in names:
+            skip = "=" not in a
+            continue
+        out.append(a)
+    return out
+
+
 def launch_dp(argv: list[str], cfg: ServerConfig) -> int:
     """``--scatter rccl``: rank 0 (this node's one front-end) + a follower per further GPU in
     one torch.distributed group on 127.0.0.1 (serving/dp.py)."""
@@ -111,7 +127,7 @@ def launch_dp(argv: list[str], cfg: ServerConfig) -> int:
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    base = [a for a in argv if not a.startswith(("--dp_rank", "--dp_world", "--procs", "--gpu_index"))]
+    base = strip_flags(argv, ("--dp_rank", "--dp_world", "--procs", "--gpu_index"))
     kids = []
     for r in range(cfg.dp_world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
@@ -130,7 +146,7 @@ def launch_procs(argv: list[str], cfg: ServerConfig) -> int:
     exits with that child's status, so the pod restarts as a whole (k8s restartPolicy)."""
     if cfg.port == 0 or cfg.rest_api_port < 0:
         raise SystemExit("--procs needs fixed ports (every process binds the same one)")
-    base = [a for a in argv if not a.startswith(("--procs", "--gpu_index"))]
+    base = strip_flags(argv, ("--procs", "--gpu_index"))
     kids = [subprocess.Popen([sys.executable, "-m", "kdl.serving", *base, "--procs=1", f"--gpu_index={i}"])
             for i in range(cfg.procs)]
     log.info("kdl model server: %d processes (pids %s) sharing gRPC :%d / REST :%d", cfg.procs,

@@ -49,7 +49,9 @@ def two_procs(tmp_path):
     (base / "1" / "synthetic.json").write_text('{"seed": 0}')
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=str(ROOT))
-    p = subprocess.Popen([sys.executable, "-m", "kdl.serving", "--procs=2", f"--port={port}", "--rest_api_port=0",
+    # space-separated "--procs 2", the form README / docs/guide.md document (the
+    # launcher used to forward the stray "2" to every child, which then refused its argv)
+    p = subprocess.Popen([sys.executable, "-m", "kdl.serving", "--procs", "2", f"--port={port}", "--rest_api_port=0",
                           f"--model_base_path={base}", "--device=null", "--host=127.0.0.1",
                           "--allowed_batch_sizes=1,2,4,8"], cwd=str(ROOT), env=env,
                          stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)

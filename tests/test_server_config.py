@@ -105,3 +105,17 @@ def test_json_logs_and_stats_snapshot():
         assert stats and "counters" in stats[0] and "gauges" in stats[0]
     finally:
         logging.getLogger().handlers[:] = old
+
+
+def test_launcher_strips_both_flag_forms():
+    """--procs / --dp_world children re-parse strictly: the launcher must drop a flag's value
+    token in the space form too (kdl/serving/server.py strip_flags)."""
+    from kdl.serving.config import config_from_args
+    from kdl.serving.server import strip_flags
+    argv = ["--procs", "8", "--port=8500", "--dp_world=4", "--gpu_index", "3", "--scatter", "rccl",
+            "--dp_rank", "1", "--model_name", "m"]
+    names = ("--dp_rank", "--dp_world", "--procs", "--gpu_index")
+    out = strip_flags(argv, names)
+    assert out == ["--port=8500", "--scatter", "rccl", "--model_name", "m"]
+    cfg = config_from_args(out + ["--procs=1", "--gpu_index=0"])      # what a child parses
+    assert cfg.procs == 1 and cfg.gpu_index == 0 and cfg.port == 8500
