@@ -42,8 +42,6 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.nstore = I(d, "nstore"); a.stride = I(d, "stride", 1);
   a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out"); a.opad = I(d, "opad");
   a.dt = I(d, "dt");
-  a.px = P<const uint16_t>(d, "px");
-  a.pH = I(d, "pH"); a.pW = I(d, "pW"); a.pld = I(d, "pld"); a.ppad = I(d, "ppad");
   a.wimg = I(d, "wimg");
   a.krot = I(d, "krot");
   a.ksplit = I(d, "ksplit");
@@ -209,29 +207,6 @@ DwArgs dw_args(const py::dict& d) {
   return a;
 }
 
-// d: {"g": geometry dict (conv_args), "layers": [{x, wp, dwk, res, y, bias, relu_in}, ...],
-//     "sync": int32 device buffer, "nM", "nN", "spin_limit"}
-ChainArgs chain_args(const py::dict& d) {
-  ChainArgs c{};
-  c.g = conv_args(d["g"].cast<py::dict>());
-  const auto layers = d["layers"].cast<py::list>();
-  if (layers.size() < 1 || layers.size() > size_t(ChainArgs::MAXL)) throw std::invalid_argument("chain: 1..32 layers");
-  c.nlayers = int(layers.size());
-  for (int l = 0; l < c.nlayers; ++l) {
-    const auto L = layers[l].cast<py::dict>();
-    c.x[l] = P<const uint16_t>(L, "x"); c.wp[l] = P<const uint16_t>(L, "wp"); c.dwk[l] = P<const uint16_t>(L, "dwk");
-    c.res[l] = P<const uint16_t>(L, "res"); c.y[l] = P<uint16_t>(L, "y"); c.bias[l] = P<const float>(L, "bias");
-    if (!c.x[l] || !c.wp[l] || !c.dwk[l] || !c.y[l] || !c.bias[l]) throw std::invalid_argument("chain: null layer pointer");
-    if (I(L, "relu_in")) c.relu_in |= 1u << l;
-    const int ro = I(L, "relu_out");
-    if (ro != 0 && ro != 1) throw std::invalid_argument("chain: relu_out must be 0 or 1");
-    if (ro) c.relu_out |= 1u << l;
-  }
-  c.sync = P<int>(d, "sync");
-  c.nM = I(d, "nM"); c.nN = I(d, "nN"); c.spin_limit = I(d, "spin_limit", 1 << 22);
-  return c;
-}
-
 void chk(hipError_t e, const char* what) { check_hip(e, what); }
 
 }  // namespace
@@ -262,16 +237,6 @@ PYBIND11_MODULE(_C, m) {
     return py::make_tuple(bm, bn, th);
   });
   m.def("conv_gemm_num_configs", &conv_gemm_num_configs);
-  m.def("sepconv_chain", [](int cfg, py::dict d, uintptr_t s) {
-    const auto c = chain_args(d);
-    py::gil_scoped_release nogil;
-    chk(sepconv_chain(cfg, c, S(s)), "sepconv_chain");
-  });
-  m.def("sepconv_chain_tiles", [](int cfg, int M, int NF) {
-    int nM = 0, nN = 0;
-    if (sepconv_chain_tiles(cfg, M, NF, &nM, &nN) != 0) throw std::out_of_range("bad chain config / geometry");
-    return py::make_tuple(nM, nN);
-  });
   // raw async copy (kind: hipMemcpyKind, 1 = H2D, 2 = D2H): the pipelined ingress /
   // egress of bench.py and the serving executor without torch's per-copy bookkeeping
   m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, int kind, uintptr_t s) {
@@ -432,9 +397,6 @@ PYBIND11_MODULE(_C, m) {
         blaslt_prepare(op.bl);
         p.add(op);
       })
-      .def("add_chain", [](Program& p, const std::string& name, int cfg, py::dict d) {
-        Op op; op.kind = OP_CHAIN; op.name = name; op.cfg = cfg; op.ch = chain_args(d); p.add(op);
-      })
       .def("add_stem", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_STEM; op.name = name; op.st = stem_args(d); p.add(op);
       })
@@ -491,9 +453,6 @@ PYBIND11_MODULE(_C, m) {
         op.mem_bytes = bytes; p.add(op);
       })
       .def("set_cfg", [](Program& p, size_t i, int cfg) { p.mutable_op(i).cfg = cfg; })
-      .def("set_branch", [](Program& p, size_t i, int branch, int join) {
-        p.mutable_op(i).branch = branch; p.mutable_op(i).join = join;
-      })
       .def("cfg", [](const Program& p, size_t i) { return p.op(i).cfg; })
       .def("op_names", [](const Program& p) {
         std::vector<std::string> v;

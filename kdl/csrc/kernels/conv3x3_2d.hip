@@ -340,7 +340,7 @@ static hipError_t launch_c3(const ConvGemmArgs& a, hipStream_t s) {
   // one N tile holding all outputs, 32 input channels (the register-resident weights),
   // 3x3 'valid' stride 1, no padded output layout
   if (a.NF * 16 != BN || a.K != 9 * 32 || a.cin != 32 || a.ldx < 32 || a.stride != 1 || a.opad ||
-      a.OH != a.H - 2 || a.OW != a.W - 2 || a.M != a.B * a.OH * a.OW || a.M <= 0 || a.res || a.px || a.dt)
+      a.OH != a.H - 2 || a.OW != a.W - 2 || a.M != a.B * a.OH * a.OW || a.M <= 0 || a.res || a.dt)
     return hipErrorInvalidValue;
   const size_t smem = c3_smem<FM, FN, WGM, WGN, ST, TH, TW>();
   if (smem > 160 * 1024) return hipErrorInvalidValue;
@@ -364,7 +364,7 @@ template <int FM, int FN, int WGM, int WGN, int ST, int TH, int TW>
 static hipError_t launch_c3w(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BN = 16 * FN * WGN, NT = 64 * (WGM * WGN + 1);
   if (a.NF * 16 != BN || a.K != 9 * 32 || a.cin != 32 || a.ldx < 32 || a.stride != 1 || a.opad ||
-      a.OH != a.H - 2 || a.OW != a.W - 2 || a.M != a.B * a.OH * a.OW || a.M <= 0 || a.res || a.px || a.dt ||
+      a.OH != a.H - 2 || a.OW != a.W - 2 || a.M != a.B * a.OH * a.OW || a.M <= 0 || a.res || a.dt ||
       a.relu_out > 1)
     return hipErrorInvalidValue;
   constexpr int PS = (TH + 2) * (TW + 2), IPP = (PS + 63) / 64;

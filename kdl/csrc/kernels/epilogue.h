@@ -1,4 +1,4 @@
-// Shared conv-GEMM epilogue store (conv_gemm / gemm_pipe / sepconv_fused):
+// Shared conv-GEMM epilogue store (conv_gemm / gemm_pipe / sepconv_ws / sepconv_2d):
 // residual add, ReLU-after-residual (ResNet), and the zero-bordered output
 // layout that lets the following 3x3 'same' conv run as a bounds-check-free
 // 'valid' implicit GEMM (the 1-pixel border is zeroed once at allocation).
@@ -48,35 +48,6 @@ template <int DT = 0>
 __device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u32x4 v) {
   using E = Elt<DT>;
   if (a.relu_out >= 3) v = act_transcendental<DT>(a.relu_out, v);
-  if (a.px) {
-    // fused TF-'same' 3x3/2 max-pool of the block's main branch (out-of-range taps skipped,
-    // the odd pad bottom/right), added to this (residual conv) output
-    const int OHW = a.OH * a.OW;
-    const int b = m / OHW, rem = m - b * OHW;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
-    const uint16_t* pb = a.px + (long)b * a.pH * a.pW * a.pld + n;
-    float mx[8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) mx[d] = -INFINITY;
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      const int ih = 2 * oh - a.ppad + dy;
-      if ((unsigned)ih >= (unsigned)a.pH) continue;
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int iw = 2 * ow - a.ppad + dx;
-        if ((unsigned)iw >= (unsigned)a.pW) continue;
-        const u32x4 pv = *(const u32x4*)(pb + ((long)ih * a.pW + iw) * a.pld);
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          mx[2 * d] = fmaxf(mx[2 * d], E::lo(pv[d]));
-          mx[2 * d + 1] = fmaxf(mx[2 * d + 1], E::hi(pv[d]));
-        }
-      }
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d) v[d] = E::pack(E::lo(v[d]) + mx[2 * d], E::hi(v[d]) + mx[2 * d + 1]);
-  }
   if (a.res) {
     const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
 #pragma unroll

@@ -33,12 +33,6 @@ struct ConvGemmArgs {
                          //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
                          // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
   int dt;                // element type of x / wp / res / y: 0 bf16, 1 fp16 (MODE_PW / MODE_CONV GEMMs)
-  // optional fused TF-'same' 3x3/2 max-pool (Xception entry/exit blocks): the epilogue adds
-  // maxpool(px)[m] to the GEMM output, px = [B][pH][pW][pld] bf16, leading pad ppad. The
-  // residual 1x1/2 conv then writes the block output directly: no pool kernel, and the
-  // conv result never round-trips through HBM (epilogue.h)
-  const uint16_t* px;
-  int pH, pW, pld, ppad;
   // per-image weights (EfficientNet project conv with the SE channel scale folded in, gemm_pipe
   // only): wp points at [B][NF][K/32][64][8] and wimg is the element stride between images;
   // M tiles then never straddle two images. 0 = one weight set for every row.
@@ -70,31 +64,6 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_ws_fits(int cfg, int W);
 
-// Chained launch of fused separable convs of one geometry (the Xception middle flow): ONE
-// launch runs `nlayers` layers; its workgroups take (layer, tile) tickets from an atomic queue
-// in layer-major order and a tile of layer l starts once the three M tiles of layer l-1 whose
-// rows its 3x3 halo reads are published (write-through stores + per-(layer, M tile) counters,
-// agent-scope acquire). Deadlock-free at any residency: a ticket's dependencies were taken
-// earlier, by workgroups that are running. sepconv_chain zeroes `sync` (4 + nlayers * nM ints)
-// with a kernel of its own ahead of every chain launch.
-struct ChainArgs {
-  static constexpr int MAXL = 32;
-  ConvGemmArgs g;               // shared geometry / flags (its pointers unused)
-  const uint16_t* x[MAXL];      // per layer, in kernel arguments (uniform scalar loads)
-  const uint16_t* wp[MAXL];
-  const uint16_t* dwk[MAXL];
-  const uint16_t* res[MAXL];
-  uint16_t* y[MAXL];
-  const float* bias[MAXL];
-  unsigned relu_in;             // bit l: ReLU on layer l's input
-  unsigned relu_out;            // bit l: ReLU before layer l's residual add (ConvGemmArgs.relu_out 1)
-  int nlayers;
-  int* sync;                    // [0] queue head, [1] error (spin gave up), [4 + l * nM + mi] done N tiles
-  int nM, nN;                   // tiles per layer (host-computed from the config's tile)
-  int spin_limit;               // dependency polls before giving up (error word set, result garbage)
-};
-hipError_t sepconv_chain(int cfg, const ChainArgs& c, hipStream_t s);
-int sepconv_chain_tiles(int cfg, int M, int NF, int* nM, int* nN);
 // cfg >= C3_CFG_BASE: 3x3 'valid' conv over 2-D tiles with an LDS halo patch (MODE_CONV, cin 32 only,
 // conv3x3_2d.hip: Xception block1_conv2).
 constexpr int C3_CFG_BASE = 208;

@@ -1,12 +1,12 @@
 // Fused SeparableConv2D (+BN)(+ReLU in/out)(+residual) over 2-D SPATIAL tiles, for
 // the large-activation early flow of Xception (147x147 and 74x74 feature maps).
 //
-// Same machinery as sepconv_pipe.hip (depthwise 3x3 as a block-diagonal 16x16x144
+// Same machinery as sepconv_ws.hip (depthwise 3x3 as a block-diagonal 16x16x144
 // GEMM on the matrix cores, pointwise MFMAs, one barrier per 32-channel k-step over an
 // LDS-DMA ring), but the M tile is a TH x TW rectangle of output pixels of one image
 // instead of BM consecutive raster pixels. Why: a raster tile needs a staged band of
 // BM + 2W + 2 pixels (one halo row above and below), i.e. 4-6x the tile at W = 147,
-// which does not fit LDS, so sepconv_pipe cannot run there at all and the split path
+// which does not fit LDS, so sepconv_ws cannot run there at all and the split path
 // (dw3x3 kernel -> HBM -> pointwise GEMM) pays a full write + read of the depthwise
 // output: ~180 MB per 147x147x128 layer at batch 32. A 2-D tile stages only its
 // (TH+2) x (TW+2) halo patch (1.5x for 6x16), so the depthwise output never leaves
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void sepconv_2d_kernel(ConvGemmArgs
       toff[i][j] = BAND + qc * PL + slot * 16;
     }
   }
-  // block-diagonal B operand from a 16-byte weight entry (see sepconv_pipe.hip)
+  // block-diagonal B operand from a 16-byte weight entry (see the sepconv_ws.hip header)
   const bool wv = (p16 >> 3) == (kb & 1);
   const int e = p16 & 7;
   uint32_t sel[2][4];
@@ -774,308 +774,6 @@ __global__ __launch_bounds__(64 * (WGM * WGN + 1)) void sepconv_2dw_kernel(ConvG
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// ---------------------------------------------------------------------------
-// sepconv_2dw + the block's TF-'same' 3x3/2 max-pool + residual add in the epilogue
-// (ids S2DWP_OFFSET..). The separable conv feeding an Xception entry-block pool used to write
-// its full-resolution output (147x147x128 at batch 32: 177 MB) for pool_add to read back and
-// quarter; here a tile is defined in POOLED space -- PH x PW pooled outputs -- and computes
-// the (2PH+1) x (2PW+1) separable-conv pixels their windows cover (the one shared row /
-// column with the next tile is recomputed), reduces them through an LDS C tile and writes
-// only maxpool + residual. Window taps outside the image are skipped (TF pads with -inf);
-// the leading pad PT is 1 for 147 -> 74 and 0 for the asymmetric 74 -> 37. Every value goes
-// through the same bf16 roundings as sepconv + pool_add: results are bit-identical.
-// Structure as sepconv_2dw_kernel (resident weights, one DMA wave, compute waves), plus one
-// barrier per tile (C tile complete) that the DMA wave joins at the same point of its loop.
-template <int FM, int FN, int WGM, int WGN, int STAGES, int PH, int PW, int PT, bool RELU>
-__global__ __launch_bounds__(64 * (WGM * WGN + 1)) void sepconv_2dwp_kernel(ConvGemmArgs a) {
-  constexpr int NW = WGM * WGN;
-  constexpr int TR = 2 * PH + 1, TC = 2 * PW + 1;         // separable-conv rows / cols per tile
-  constexpr int NPIX = TR * TC;
-  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
-  static_assert(BM >= NPIX && BM - NPIX < 16 * WGM, "M tile = the region's pixels, rounded up to fragments");
-  static_assert(NW % 2 == 0 && STAGES >= 3, "a wave's depthwise units share one channel group; ring depth");
-  constexpr int PPW = TC + 2;                              // patch pitch (slots)
-  constexpr int PS = (TR + 2) * PPW;
-  constexpr int IPP = (PS + 1 + 63) / 64;
-  constexpr int ZSLOT = 64 * IPP - 1;
-  constexpr int XB = 4 * IPP;
-  constexpr int AF = BM / 16, BF = BN / 16;
-  constexpr int PL = IPP * 1024;
-  constexpr int STAGE = XB * 1024;
-  constexpr int ABUF = AF * 1024;
-  constexpr int CS = BN * 2 + 16;
-  constexpr int U = 2 * AF;
-  constexpr int UPW = (U + NW - 1) / NW;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool dma = wave == NW;
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int W = a.W, H = a.H, OH = a.OH, OW = a.OW;
-  const int KT = a.K >> 5;
-  const int ntw = (OW + PW - 1) / PW, nth = (OH + PH - 1) / PH;
-  const int ntiles = a.B * nth * ntw;
-  const int G = gridDim.x;
-  const int t0 = xcd_remap(blockIdx.x, G);
-  const int TWn = t0 < ntiles ? (ntiles - t0 + G - 1) / G : 0;
-  const int Q = TWn * KT;
-  if (Q == 0) return;
-  uint8_t* const bres = smem;
-  uint8_t* const dres = smem + KT * BF * 1024;
-  uint8_t* const ring = dres + KT * 1024;
-  uint8_t* const abuf = ring + STAGES * STAGE;
-  uint8_t* const ctile = abuf + 2 * ABUF;
-
-  for (int idx = wave; idx < KT * BF; idx += NW + 1) {
-    const int k = idx / BF, f = idx - k * BF;
-    glds16(a.wp + ((long)f * KT + k) * 512 + lane * 8, bres + idx * 1024);
-  }
-  for (int k = wave; k < KT; k += NW + 1) glds16((const uint8_t*)a.dwk + k * 1024 + lane * 16, dres + k * 1024);
-
-  auto tile_origin = [&](int ti, int& bimg, int& ph0, int& pw0) {
-    const int tile = t0 + ti * G;
-    bimg = tile / (nth * ntw);
-    const int trem = tile - bimg * (nth * ntw);
-    ph0 = (trem / ntw) * PH;
-    pw0 = (trem % ntw) * PW;
-  };
-
-  if (dma) {
-    int iq = 0, ik = 0, iti = 0;
-    const uint8_t* psrc[XB];
-    auto enter_tile = [&](int ti) {
-      int bimg, ph0, pw0;
-      tile_origin(ti, bimg, ph0, pw0);
-      const int r0 = 2 * ph0 - PT, c0 = 2 * pw0 - PT;     // region origin (separable-conv pixels)
-#pragma unroll
-      for (int sidx = 0; sidx < XB; ++sidx) {
-        const int q = sidx / IPP, slot = (sidx % IPP) * 64 + lane;
-        const int pr = slot / PPW, pc = slot - pr * PPW;
-        const int h = r0 - 1 + pr, w = c0 - 1 + pc;
-        const bool in = slot < PS && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-        psrc[sidx] = in ? (const uint8_t*)(a.x + (((long)bimg * H + h) * W + w) * a.ldx + q * 8) : s2d_zeros;
-      }
-    };
-    auto issue = [&](int slotbuf) {
-      uint8_t* base = ring + slotbuf * STAGE;
-#pragma unroll
-      for (int sidx = 0; sidx < XB; ++sidx) glds16(psrc[sidx] + ik * 64, base + sidx * 1024);
-      if (iq + 1 < Q) {
-        ++iq;
-        if (++ik == KT) {
-          ik = 0;
-          enter_tile(++iti);
-        }
-      }
-    };
-    enter_tile(0);
-    for (int p = 0; p < STAGES - 1; ++p) issue(p);
-    s2_wait_barrier<(STAGES - 2) * XB>();
-    for (int q = 0; q < Q; ++q) {
-      s2_wait_barrier<(STAGES - 3) * XB>();
-      issue((q + STAGES - 1) % STAGES);
-      if ((q + 1) % KT == 0) s2_wait_barrier<63>();      // the compute waves' C-tile barrier
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-
-  const int g = wave & 1;
-  const int p16 = lane & 15, kb = lane >> 4;
-  const int par = kb >> 1;
-  const int qc = 2 * g + (kb & 1);
-  const int ulast = U - 1 - ((U - 1 - wave) & 1);
-  int toff[UPW][5];
-#pragma unroll
-  for (int i = 0; i < UPW; ++i) {
-    const int u = min(wave + NW * i, ulast);
-    const int pix = min((u >> 1) * 16 + p16, NPIX - 1);   // padding rows recompute the last pixel
-    const int r = pix / TC, c = pix - r * TC;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int tap = 2 * j + par;
-      const int slot = tap < 9 ? (r + tap / 3) * PPW + c + tap % 3 : ZSLOT;
-      toff[i][j] = qc * PL + slot * 16;
-    }
-  }
-  const bool wv = (p16 >> 3) == (kb & 1);
-  const int e = p16 & 7;
-  uint32_t sel[2][4];
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t pair = (2u * jp) | ((2u * jp + 1u) << 8);
-      const uint32_t val = (e & 1) ? (0x0c0cu | (pair << 16)) : (0x0c0c0000u | pair);
-      sel[jp][d] = (wv && (e >> 1) == d) ? val : 0x0c0c0c0cu;
-    }
-  const int went = ((g * 16 + p16) * 2 + par) * 16;
-  const int aoffw = (p16 + 16 * (2 * g + (kb >> 1))) * 16 + 8 * (kb & 1);
-  const int quad = lane >> 4, col = lane & 15;
-  float4 bvr[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) bvr[j] = *(const float4*)(a.bias + wn * FN * 16 + j * 16 + 4 * quad);
-
-  auto dw_load = [&](int slotbuf, int k, u32x4 (&xv)[UPW][5]) -> u32x4 {
-    const uint8_t* sb = ring + slotbuf * STAGE;
-#pragma unroll
-    for (int i = 0; i < UPW; ++i)
-#pragma unroll
-      for (int j = 0; j < 5; ++j) xv[i][j] = *(const u32x4*)(sb + toff[i][j]);
-    return *(const u32x4*)(dres + k * 1024 + went);
-  };
-  auto dw_mfma = [&](const u32x4 we, u32x4 (&xv)[UPW][5], int ab) {
-    s16x8 wf[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const uint32_t wd = we[j >> 1];
-      u32x4 f;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) f[d] = __builtin_amdgcn_perm(wd, wd, sel[j & 1][d]);
-      wf[j] = __builtin_bit_cast(s16x8, f);
-    }
-    f32x4 dacc[UPW];
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) dacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-#pragma unroll
-      for (int i = 0; i < UPW; ++i) {
-        u32x4 v = xv[i][j];
-        if constexpr (RELU) {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
-        }
-        dacc[i] = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc[i]);
-      }
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-      const int u = min(wave + NW * i, ulast);
-      *(u32x2*)(abuf + ab * ABUF + (u >> 1) * 1024 + aoffw) =
-          (u32x2){pack_bf16(dacc[i][0], dacc[i][1]), pack_bf16(dacc[i][2], dacc[i][3])};
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  s2_wait_barrier<0>();
-  {
-    u32x4 xv[UPW][5];
-    const u32x4 we = dw_load(0, 0, xv);
-    dw_mfma(we, xv, 0);
-  }
-  int k = 0, ti = 0;
-  for (int q = 0; q < Q; ++q) {
-    s2_wait_barrier<63>();
-    const uint8_t* As = abuf + (q & 1) * ABUF + lane * 16;
-    const uint8_t* Bs = bres + k * BF * 1024 + lane * 16;
-    s16x8 af[FM], bf[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(As + (wm * FM + i) * 1024);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(Bs + (wn * FN + j) * 1024);
-    const int k1 = k + 1 == KT ? 0 : k + 1;
-    u32x4 xv[UPW][5];
-    const u32x4 we = dw_load((q + 1) % STAGES, k1, xv);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
-    dw_mfma(we, xv, (q + 1) & 1);
-    __builtin_amdgcn_s_setprio(0);
-    if (k1 == 0) {
-      // ---- tile epilogue: bias (+ReLU) -> bf16 C tile (region pixel x channel) in LDS
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int nl = wn * FN * 16 + j * 16 + 4 * quad;
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int mll = (wm * FM + i) * 16 + col;
-          float v0 = acc[i][j][0] + bvr[j].x, v1 = acc[i][j][1] + bvr[j].y;
-          float v2 = acc[i][j][2] + bvr[j].z, v3 = acc[i][j][3] + bvr[j].w;
-          if (a.relu_out == 1) {
-            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-          }
-          *(u32x2*)(ctile + mll * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
-          acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      s2_wait_barrier<63>();                   // C tile complete (the DMA wave joins this barrier)
-      // ---- 3x3/2 max over the tile's windows (+ residual) -> pooled output, 16 B per item
-      int bimg, ph0, pw0;
-      tile_origin(ti, bimg, ph0, pw0);
-      const int r0 = 2 * ph0 - PT, c0 = 2 * pw0 - PT;
-      constexpr int CPI = BN / 8;              // 8-channel chunks per pooled pixel
-      for (int it = tid; it < PH * PW * CPI; it += NW * 64) {
-        const int pp = it / CPI, cc = it - pp * CPI;
-        const int py = pp / PW, px = pp - py * PW;
-        const int oh = ph0 + py, ow = pw0 + px;
-        if (oh >= OH || ow >= OW) continue;
-        float mx[8];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) mx[d] = -INFINITY;
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const int r = 2 * py + dy;
-          if ((unsigned)(r0 + r) >= (unsigned)H) continue;
-#pragma unroll
-          for (int dx = 0; dx < 3; ++dx) {
-            const int c = 2 * px + dx;
-            if ((unsigned)(c0 + c) >= (unsigned)W) continue;
-            const u32x4 v = *(const u32x4*)(ctile + (r * TC + c) * CS + cc * 16);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-              mx[2 * d] = fmaxf(mx[2 * d], bf_lo(v[d]));
-              mx[2 * d + 1] = fmaxf(mx[2 * d + 1], bf_hi(v[d]));
-            }
-          }
-        }
-        const long op = ((long)bimg * OH + oh) * OW + ow;
-        if (a.res) {
-          const u32x4 rv = *(const u32x4*)(a.res + op * a.ldr + cc * 8);
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            mx[2 * d] += bf_lo(rv[d]);
-            mx[2 * d + 1] += bf_hi(rv[d]);
-          }
-        }
-        if (cc * 8 < a.nstore) {
-          u32x4 o;
-#pragma unroll
-          for (int d = 0; d < 4; ++d) o[d] = pack_bf16(mx[2 * d], mx[2 * d + 1]);
-          *(u32x4*)(a.y + op * a.ldy + cc * 8) = o;
-        }
-      }
-      ++ti;
-    }
-    k = k1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// (FM, FN, WGM, WGN, STAGES, PH, PW, PT) of the pooled DMA-wave variant; ids S2D_CFG_BASE +
-// S2DWP_OFFSET + i (host ids 205..207). FM * WGM fragments cover (2PH+1) x (2PW+1) pixels.
-constexpr int S2DWP_OFFSET = 45;
-#define KDL_S2DWP_CONFIGS(X)       \
-  X(0, 5, 2, 2, 4, 3, 4, 8, 1)     \
-  X(1, 5, 2, 2, 4, 3, 4, 8, 0)     \
-  X(2, 3, 2, 2, 4, 4, 2, 8, 1)
-
-template <int FM, int FN, int WGM, int WGN, int ST, int PH, int PW, int PT>
-static size_t s2dwp_smem(int K) {
-  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
-  constexpr int PS = (2 * PH + 3) * (2 * PW + 3), IPP = (PS + 1 + 63) / 64;
-  const int KT = K / 32;
-  return (size_t)KT * (BN / 16) * 1024 + (size_t)KT * 1024 + (size_t)ST * 4 * IPP * 1024 + 2 * (BM / 16) * 1024 +
-         (size_t)BM * (BN * 2 + 16);
-}
-
 // (FM, FN, WGM, WGN, STAGES, TH, TW) of the persistent variant; ids S2D_CFG_BASE + S2DP_OFFSET + i.
 constexpr int S2DP_OFFSET = 24;
 #define KDL_S2DP_CONFIGS(X)     \
@@ -1090,7 +788,7 @@ constexpr int S2DP_OFFSET = 24;
   X(8, 3, 2, 2, 4, 7, 6, 16)
 
 // (FM, FN, WGM, WGN, STAGES, TH, TW) of the DMA-wave variant; ids S2D_CFG_BASE + S2DW_OFFSET + i
-// (host ids 200..207: C3_CFG_BASE = 208 follows).
+// (host ids 200..204; 205..207 retired: the round-3 pooled variant; C3_CFG_BASE = 208 follows).
 constexpr int S2DW_OFFSET = 40;
 #define KDL_S2DW_CONFIGS(X)     \
   X(0, 2, 2, 2, 4, 4, 4, 16)    \
@@ -1105,31 +803,13 @@ template <int FM, int FN, int WGM, int WGN, int ST, int TH, int TW>
 static hipError_t launch_s2dw(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN, NT = 64 * (WGM * WGN + 1);
   using P = S2dPatch<TH, TW>;
-  if (a.NF * 16 != BN || a.px || a.opad || a.relu_out > 2 || a.dt) return hipErrorInvalidValue;
+  if (a.NF * 16 != BN || a.opad || a.relu_out > 2 || a.dt) return hipErrorInvalidValue;
   const int KT = a.K / 32;
   const size_t smem = (size_t)KT * (BN / 16) * 1024 + (size_t)KT * 1024 + (size_t)ST * P::XB * 1024 + 2 * (BM / 16) * 1024;
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   const int ntiles = a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
   auto kern = a.relu_in ? sepconv_2dw_kernel<FM, FN, WGM, WGN, ST, TH, TW, true>
                         : sepconv_2dw_kernel<FM, FN, WGM, WGN, ST, TH, TW, false>;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, smem) != hipSuccess || per_cu <= 0) per_cu = 1;
-  const int grid = std::min(ntiles, s2dp_num_cus() * per_cu);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), smem, s, a);
-  return hipGetLastError();
-}
-
-template <int FM, int FN, int WGM, int WGN, int ST, int PH, int PW, int PT>
-static hipError_t launch_s2dwp(const ConvGemmArgs& a, hipStream_t s) {
-  constexpr int BN = 16 * FN * WGN, NT = 64 * (WGM * WGN + 1);
-  // pooled-space geometry: OH / OW are the pooled output, a.ppad its leading pad; one N tile
-  if (a.NF * 16 != BN || a.ppad != PT || a.opad || a.relu_out > 1 || a.dt || a.px) return hipErrorInvalidValue;
-  if (a.OH != (a.H - 1) / 2 + 1 || a.OW != (a.W - 1) / 2 + 1 || a.M != a.B * a.OH * a.OW) return hipErrorInvalidValue;
-  const size_t smem = s2dwp_smem<FM, FN, WGM, WGN, ST, PH, PW, PT>(a.K);
-  if (smem > 160 * 1024) return hipErrorInvalidValue;
-  const int ntiles = a.B * ((a.OH + PH - 1) / PH) * ((a.OW + PW - 1) / PW);
-  auto kern = a.relu_in ? sepconv_2dwp_kernel<FM, FN, WGM, WGN, ST, PH, PW, PT, true>
-                        : sepconv_2dwp_kernel<FM, FN, WGM, WGN, ST, PH, PW, PT, false>;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, smem) != hipSuccess || per_cu <= 0) per_cu = 1;
   const int grid = std::min(ntiles, s2dp_num_cus() * per_cu);
@@ -1190,15 +870,6 @@ static hipError_t launch_s2dp(const ConvGemmArgs& a, hipStream_t s) {
   X(13, 3, 4, 2, 4, 4, 6, 16)
 
 int sepconv_2d_config(int cfg, int* bm, int* bn, int* threads) {
-  if (cfg >= S2DWP_OFFSET) {
-    switch (cfg - S2DWP_OFFSET) {
-#define KDL_S2WPINFO(id, fm, fn, wgm, wgn, st, ph, pw, pt) \
-  case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * (wgm * wgn + 1); return 0;
-      KDL_S2DWP_CONFIGS(KDL_S2WPINFO)
-#undef KDL_S2WPINFO
-      default: return -1;
-    }
-  }
   if (cfg >= S2DW_OFFSET) {
     switch (cfg - S2DW_OFFSET) {
 #define KDL_S2WINFO(id, fm, fn, wgm, wgn, st, th, tw) \
@@ -1228,17 +899,6 @@ int sepconv_2d_config(int cfg, int* bm, int* bn, int* threads) {
 
 hipError_t sepconv_2d(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   int bm, bn, th;
-  if (cfg >= S2DWP_OFFSET) {                  // separable conv + block max-pool + residual: pooled geometry
-    if (sepconv_2d_config(cfg, &bm, &bn, &th) != 0 || a.K % 32 != 0 || a.K > 8192 || a.M <= 0 || a.dwk == nullptr)
-      return hipErrorInvalidValue;
-    switch (cfg - S2DWP_OFFSET) {
-#define KDL_S2WPCASE(id, fm, fn, wgm, wgn, st, ph, pw, pt) \
-  case id: return launch_s2dwp<fm, fn, wgm, wgn, st, ph, pw, pt>(a, s);
-      KDL_S2DWP_CONFIGS(KDL_S2WPCASE)
-#undef KDL_S2WPCASE
-      default: return hipErrorInvalidValue;
-    }
-  }
   if (sepconv_2d_config(cfg, &bm, &bn, &th) != 0 || a.K % 32 != 0 || a.K > 8192 || (a.NF * 16) % bn != 0 ||
       a.OH != a.H || a.OW != a.W || a.M != a.B * a.H * a.W || a.M <= 0 || a.dwk == nullptr)
     return hipErrorInvalidValue;

@@ -29,7 +29,6 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_CHSCALE: return channel_scale(op.cs, s);
     case OP_WSCALE: return weight_scale(op.ws, s);
     case OP_GEMM_F8: return gemm_f8(op.cfg, op.f8, s);
-    case OP_CHAIN: return sepconv_chain(op.cfg, op.ch, s);
     case OP_BLASLT: return blaslt_run(op.bl, s);
   }
   return hipErrorInvalidValue;
@@ -50,46 +49,15 @@ void Program::run(hipStream_t s) const {
 
 void Program::capture(hipStream_t s) {
   reset();
-  const bool branches = std::any_of(ops_.begin(), ops_.end(), [](const Op& o) { return o.branch != 0; });
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  if (branches) {
-    check_hip(hipStreamCreateWithFlags(&side, hipStreamNonBlocking), "hipStreamCreate(side)");
-    check_hip(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming), "hipEventCreate");
-    check_hip(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming), "hipEventCreate");
-  }
   check_hip(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
   hipError_t err = hipSuccess;
   std::string bad;
-  bool forked = false;
-  auto join = [&]() {
-    if (!forked) return hipSuccess;
-    forked = false;
-    hipError_t e = hipEventRecord(join_ev, side);
-    return e != hipSuccess ? e : hipStreamWaitEvent(s, join_ev, 0);
-  };
   for (const auto& op : ops_) {
-    if (op.branch) {
-      if (!forked) {     // the side branch sees everything the main stream issued so far
-        err = hipEventRecord(fork_ev, s);
-        if (err == hipSuccess) err = hipStreamWaitEvent(side, fork_ev, 0);
-        forked = true;
-      }
-      if (err == hipSuccess) err = run_op(op, side);
-    } else {
-      if (op.join) err = join();
-      if (err == hipSuccess) err = run_op(op, s);
-    }
+    err = run_op(op, s);
     if (err != hipSuccess) { bad = op.name; break; }
   }
-  if (err == hipSuccess) err = join();      // a dangling branch joins at the end
   hipGraph_t g = nullptr;
   const hipError_t e2 = hipStreamEndCapture(s, &g);
-  if (side) {
-    (void)hipEventDestroy(fork_ev);
-    (void)hipEventDestroy(join_ev);
-    (void)hipStreamDestroy(side);
-  }
   if (err != hipSuccess) {
     if (g) (void)hipGraphDestroy(g);
     check_hip(err, "capture launch " + bad);

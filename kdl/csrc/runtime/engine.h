@@ -19,7 +19,7 @@ namespace kdl {
 enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6, OP_GAP = 7, OP_FC = 8, OP_FC_MFMA = 9,
               OP_PATCHIFY = 10, OP_EMBED = 11, OP_LN = 12, OP_ATTN = 13,
               OP_DWK = 14, OP_SE = 15, OP_CHSCALE = 16, OP_GEMM_F8 = 17, OP_WSCALE = 18,
-              OP_CHAIN = 19, OP_BLASLT = 20 };
+              OP_BLASLT = 20 };   // 19: retired (the round-3 chained middle-flow launch)
 
 struct Op {
   OpKind kind;
@@ -43,15 +43,9 @@ struct Op {
   ChScaleArgs cs{};
   WScaleArgs ws{};
   GemmF8Args f8{};
-  ChainArgs ch{};
   BlasLtArgs bl{};   // OP_BLASLT: plan built at add time (blaslt_prepare)
   void* mem_ptr = nullptr;
   size_t mem_bytes = 0;
-  // graph-level concurrency (capture only; eager runs stay sequential): branch = 1 ops
-  // run on a side stream forked from the main one at the first such op; join = 1 makes
-  // this (main-stream) op wait for the side branch (Xception: the residual 1x1 conv of
-  // an entry/exit block runs beside the block's separable convs, joined at the pool)
-  int branch = 0, join = 0;
 };
 
 void check_hip(hipError_t e, const std::string& what);

@@ -10,6 +10,7 @@ TF-Serving servable's session run (`tf-serving.dockerfile:2-5`)
 """
 from __future__ import annotations
 
+import contextlib
 import json
 from dataclasses import dataclass, field
 from pathlib import Path
@@ -84,7 +85,7 @@ class EngineBase:
     # ---------------------------------------------------------------- programs
     def conv_steps(self) -> list[Step]:
         """Steps with a tunable GEMM layer (bf16 conv-GEMM or fp8 linear)."""
-        return [s for s in self.steps if s.kind in ("conv", "convpool", "f8")]
+        return [s for s in self.steps if s.kind in ("conv", "f8")]
 
     def program(self, b: int, capture: bool = True, slot: int = 0):
         key = (b, capture, slot)
@@ -137,37 +138,13 @@ class EngineBase:
         return prog
 
     def _emit_steps(self, prog, steps: list[Step], maps: list[dict], b: int) -> None:
-        """Emit a run of steps (each with its buffer remap). Runs that ``_chain_end`` groups
-        become ONE chained launch (``_emit_chain``); a program range never chains across its
-        ends, so a stage cut (stages.py) always falls between launches."""
-        i = 0
-        while i < len(steps):
-            j = self._chain_end(steps, i)
-            if j - i >= 2:
-                self._emit_chain(prog, steps[i:j], maps[i:j], b)
-                i = j
-                continue
-            self._remap = maps[i]
-            self._emit_marked(prog, steps[i], b)
-            i += 1
-
-    def _chain_end(self, steps: list[Step], i: int) -> int:
-        """End (exclusive) of the chainable run starting at steps[i]; <= i + 1: no chain."""
-        return i + 1
-
-    def _emit_chain(self, prog, steps: list[Step], maps: list[dict], b: int) -> None:
-        raise NotImplementedError
-
-    def _emit_marked(self, prog, step: Step, b: int) -> None:
-        """Emit one step and carry its graph-concurrency marks onto its ops: extra
-        ``branch`` = the step's ops run on the captured graph's side branch, ``join`` =
-        the step waits for that branch first (native Program.capture)."""
-        n0 = len(prog)
-        self._emit(prog, step, b)
-        br, jn = int(step.extra.get("branch", 0)), int(step.extra.get("join", 0))
-        if br or jn:
-            for i in range(n0, len(prog)):
-                prog.set_branch(i, br, jn if i == n0 else 0)
+        """Emit a run of steps, each with its buffer remap, on the engine's device (a vendor
+        GEMM node builds its plan and workspace for the CURRENT device at emission time)."""
+        ctx = torch.cuda.device(self.device) if self.device.type == "cuda" else contextlib.nullcontext()
+        with ctx:
+            for st, m in zip(steps, maps):
+                self._remap = m
+                self._emit(prog, st, b)
 
     def invalidate(self) -> None:
         self.programs.clear()

@@ -54,9 +54,7 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            189: (2, 4, 2, 4), 190: (2, 2, 2, 4), 191: (2, 2, 2, 4), 192: (3, 2, 2, 4),
            # persistent 2-D sepconv with a dedicated DMA wave, direct stores (KDL_S2DW_CONFIGS)
            200: (2, 2, 2, 4), 201: (4, 2, 2, 4), 202: (3, 2, 2, 4), 203: (2, 4, 2, 4), 204: (4, 2, 2, 4),
-           # ... + the block's 3x3/2 max-pool and residual add in the epilogue (sepconv_2dwp_kernel,
-           # KDL_S2DWP_CONFIGS): a "seppool" step only, never an ordinary separable-conv candidate
-           205: (5, 2, 2, 4), 206: (5, 2, 2, 4), 207: (3, 2, 2, 4),
+           # 205-207 retired (round 3's pooled variant, measured slower)
            # 3x3 'valid' conv over 2-D tiles, LDS halo patch, cin 32 (conv3x3_2d.hip, KDL_C3_CONFIGS)
            208: (2, 2, 4, 2), 209: (1, 2, 4, 2), 210: (2, 2, 4, 2), 211: (3, 2, 4, 2),
            # ... with a dedicated DMA wave, accumulators stored directly (conv3x3_2dw_kernel)
@@ -66,8 +64,6 @@ S2DP = {184: (4, 6, 16), 185: (4, 4, 16), 186: (3, 4, 16), 187: (4, 8, 16), 188:
         190: (8, 4, 16), 191: (11, 4, 16), 192: (7, 6, 16)}
 # DMA-wave variant (sepconv_2dw_kernel): no C tile / bias in LDS
 S2DW = {200: (4, 4, 16), 201: (4, 8, 16), 202: (4, 6, 16), 203: (4, 4, 16), 204: (6, 8, 16)}
-# pooled DMA-wave variant: (STAGES, PH, PW, leading pool pad) per id (mirror of KDL_S2DWP_CONFIGS)
-S2DWP = {205: (3, 4, 8, 1), 206: (3, 4, 8, 0), 207: (4, 2, 8, 1)}
 SEP_BASE = 64
 SEPW_BASE = 120   # warp-specialized variant (sepconv_ws.hip)
 S2D_BASE = 160    # 2-D spatial tiles (sepconv_2d.hip): the early flow's 147x147 / 74x74 maps
@@ -84,10 +80,8 @@ BLT_ALGOS = 6
 # ids >= SPLITK_BASE: an LDS-DMA GEMM config (16..63) with K split over ksplit workgroups per tile
 # (gemm_pipe.hip ConvGemmArgs.ksplit): SPLITK_BASE + 100 * ksplit + base id
 SPLITK_BASE = 2000
-# ws configs with a chained (multi-layer, one launch) variant: sepconv_ws.hip KDL_CHAIN_CONFIGS
-CHAIN_CONFIGS = (143, 144, 146)
-# never autotune candidates: the ws stamping build and band ablation, the pooled sepconv (seppool only)
-ABLATION_IDS = frozenset([127, 147] + list(S2DWP))
+# never autotune candidates: the ws stamping build and band ablation
+ABLATION_IDS = frozenset([127, 147])
 
 
 def s2dp_smem(cfg: int, K: int) -> int:
@@ -101,27 +95,8 @@ def s2dp_smem(cfg: int, K: int) -> int:
     return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024 + bm * (bn * 2 + 16) + 1024
 
 
-def s2dwp_smem(cfg: int, K: int) -> int:
-    """LDS bytes of a pooled separable config (mirror of s2dwp_smem in sepconv_2d.hip)."""
-    st, ph, pw, _ = S2DWP[cfg]
-    bm, bn = cfg_tile(cfg)
-    ps = (2 * ph + 3) * (2 * pw + 3)
-    ipp = (ps + 1 + 63) // 64
-    kt = K // 32
-    return kt * (bn // 16) * 1024 + kt * 1024 + st * 4 * ipp * 1024 + 2 * (bm // 16) * 1024 + bm * (bn * 2 + 16)
-
-
-def pool_configs(K: int, n: int, pad: int) -> list[int]:
-    """Pooled separable configs (sepconv + 3x3/2 max-pool + residual in one kernel) that fit a
-    layer: one N tile of all outputs, resident weights within LDS, matching leading pool pad."""
-    return [c for c, (_, _, _, pt) in sorted(S2DWP.items())
-            if pt == pad and round_up(n, cfg_tile(c)[1]) == cfg_tile(c)[1] and s2dwp_smem(c, K) <= 160 * 1024]
-
-
 def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | None = None) -> bool:
     """Mirror of the host-side launch checks in sepconv_ws.hip / sepconv_2d.hip / conv3x3_2d.hip."""
-    if cfg in S2DWP:      # pooled variant: only through a "seppool" step (pool_configs)
-        return False
     if cfg >= C3_BASE:    # one N tile of all outputs, 32 input channels (K = 288)
         return (K is None or K == 288) and (n is None or round_up(n, cfg_tile(cfg)[1]) == cfg_tile(cfg)[1])
     if cfg < SEP_BASE or W is None:
@@ -282,20 +257,17 @@ class ConvGemmLayer:
 
     def emit(self, prog, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
              ldr: int | None = None, tmp: int | None = None, split: bool | None = None,
-             cfg: int | None = None, opad: int = 0, pool: dict | None = None,
+             cfg: int | None = None, opad: int = 0,
              wimg: tuple[int, int] | None = None) -> None:
         """Append this layer's launches to a native Program (or launch now if prog is None).
-        ``pool``: fused 3x3/2 max-pool added in the epilogue (MODE_PW only), dict(px, pH, pW,
-        pld, ppad) -- see ConvGemmArgs.px. ``wimg``: (pointer, per-image element stride) of
+        ``wimg``: (pointer, per-image element stride) of
         per-image copies of the packed weights (ConvGemmArgs.wimg; LDS-DMA GEMM configs only)."""
         split = self.split if split is None else split
         cfg = self.cfg if cfg is None else cfg
         if is_blaslt(cfg):
-            assert pool is None and wimg is None and not split
+            assert wimg is None and not split
             self._emit_blaslt(prog, x, y, g, res, ldx, ldr, cfg, opad)
             return
-        assert pool is None or self.mode == MODE_PW or cfg in S2DWP, \
-            "the pool epilogue rides a pointwise GEMM or a pooled separable config"
         C = _lib.lib()
         if self.mode == MODE_DW and split:
             assert tmp is not None, "split separable conv needs a scratch buffer"
@@ -311,7 +283,7 @@ class ConvGemmLayer:
             return
         if is_splitk(cfg):
             sk, cfg = splitk_parts(cfg)
-            assert pool is None and wimg is None and (self.K // 32) % sk == 0, (self.name, sk)
+            assert wimg is None and (self.K // 32) % sk == 0, (self.name, sk)
             ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
             ws, cnt = self._splitk_workspace(sk, cfg, g.M)
             ga.update(ksplit=sk, ws=_lib.ptr(ws), cnt=_lib.ptr(cnt))
@@ -321,8 +293,6 @@ class ConvGemmLayer:
                 prog.add_conv_gemm(self.name, self.mode, cfg, ga)
             return
         ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
-        if pool:
-            ga.update(pool)
         if wimg:
             assert PIPE_BASE <= cfg < SEP_BASE, "per-image weights ride the LDS-DMA pipelined GEMM"
             ga.update(wp=wimg[0], wimg=wimg[1])

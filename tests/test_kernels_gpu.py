@@ -272,31 +272,6 @@ def test_pool_add_batch_beyond_grid_y_limit():
     assert (y.float().view(-1, C) - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("H,cin,C", [(147, 64, 128), (74, 128, 256), (37, 256, 736), (19, 736, 1024)])
-def test_pointwise_pool_epilogue(H, cin, C):
-    """Residual 1x1/2 conv with the block's TF-'same' 3x3/2 max-pool fused into its epilogue
-    (ConvGemmArgs.px, the Xception "convpool" step) == conv -> pool_add, every tile config."""
-    from kdl.models.layers import tf_same_pad
-    gen = torch.Generator().manual_seed(8)
-    B = 2
-    OH, pt, _ = tf_same_pad(H, 3, 2)
-    lay = _layer(MODE_PW, cin, C, gen, stride=2)
-    assert lay.ldy == C
-    g = Geometry(B, H, H, OH, OH)
-    x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
-    main = torch.randn(B * H * H * C, generator=gen).to(torch.bfloat16).to(DEV)
-    conv = conv_gemm_ref(lay, x, g).to(torch.bfloat16).to(DEV).contiguous()
-    ref = pool_add_ref(main, conv.view(-1), B, H, H, OH, OH, C, pt)
-    pool = dict(px=_lib.ptr(main), pH=H, pW=H, pld=C, ppad=pt)
-    for _, cfg in lay.variants(H):
-        y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
-        lay.check(x, y, g)
-        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=cfg, pool=pool)
-        torch.cuda.synchronize()
-        err = (y.float().view(-1, C) - ref).abs().max().item()
-        assert err <= 2e-2 * ref.abs().max().item(), (cfg, err)
-
-
 @pytest.mark.parametrize("HW,K,N", [(37 * 37, 480, 80), (19 * 19, 2304, 384), (150 * 150 // 9, 288, 48)])
 def test_per_image_weights_fold_channel_scale(HW, K, N):
     """EfficientNet SE fold: weight_scale makes per-image copies of the packed project weights
@@ -345,123 +320,3 @@ def test_head():
     torch.cuda.synchronize()
     ref = head_ref(x, B, HW, F_, F_, w1, b1, w2, b2)
     assert torch.allclose(out, ref, atol=1e-4, rtol=1e-3), (out - ref).abs().max()
-
-
-@pytest.mark.parametrize("H,cfg,with_res", [(147, 205, True), (147, 207, True), (74, 206, True), (37, 205, False),
-                                            (19, 207, True), (20, 206, True), (18, 206, True)])
-def test_sepconv_pool_fused_matches_unfused(H, cfg, with_res):
-    """sepconv_2dwp (separable conv + TF-'same' 3x3/2 max-pool + residual in one kernel) against
-    the fp32 reference of conv -> pool_add, every pad case (147 -> 74 and odd sizes pad 1,
-    74 -> 37 / even sizes pad 0), partial pooled tiles at both edges; and BIT-identical to the
-    unfused HIP path (sepconv_2dw, same accumulation order, + pool_add) where that runs."""
-    from kdl.models.layers import tf_same_pad
-    from kdl.ops.conv import S2DWP
-    gen = torch.Generator().manual_seed(31)
-    lay = _layer(MODE_DW, 128, 128, gen, relu_in=True, relu_out=False)
-    B = 2
-    OH, pt, _ = tf_same_pad(H, 3, 2)
-    if S2DWP[cfg][3] != pt:
-        pytest.skip("config for the other pad")
-    x = _rand_act((B, H, H), lay.cin_pad, 128, gen)
-    res = _rand_act((B, OH, OH), lay.ldy, 128, gen) if with_res else None
-    y = torch.full((B * OH * OH * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
-    lay.emit(None, _lib.ptr(x), _lib.ptr(y), Geometry(B, H, H, OH, OH), res=_lib.ptr(res), ldr=lay.ldy, cfg=cfg,
-             pool=dict(ppad=pt))
-    torch.cuda.synchronize()
-    full = conv_gemm_ref(lay, x, Geometry(B, H, H, H, H))            # fp32 [M][ldy] of the separable conv
-    ref = pool_add_ref(full.to(torch.bfloat16).reshape(-1).to(DEV), res, B, H, H, OH, OH, lay.ldy, pt)
-    err = (y.float().view(-1, lay.ldy) - ref.view(-1, lay.ldy)).abs().max().item()
-    assert err <= 2e-2 * ref.abs().max().item(), err
-    if H >= 64:                                  # the unfused HIP path with the same arithmetic
-        yf = torch.zeros(B * H * H * lay.ldy, dtype=torch.bfloat16, device=DEV)
-        lay.launch(x, yf, Geometry(B, H, H, H, H), cfg=204)
-        y2 = torch.zeros_like(y)
-        _lib.lib().pool_add(dict(x=_lib.ptr(yf), res=_lib.ptr(res), y=_lib.ptr(y2), B=B, H=H, W=H, OH=OH, OW=OH,
-                                 C=lay.ldy, pad_top=pt, pad_left=pt), _lib.stream_ptr())
-        torch.cuda.synchronize()
-        assert torch.equal(y, y2)
-
-
-def test_xception_seppool_lowering_is_bit_identical(xparams):
-    """KDL_SEP_POOL: block2's last separable conv + pool_add as one seppool step gives exactly the
-    logits of the unfused lowering (same sepconv_2dw arithmetic, same bf16 roundings)."""
-    import os
-    from kdl.engine.xception import XceptionEngine
-    old = os.environ.get("KDL_SEP_POOL")
-    try:
-        os.environ["KDL_SEP_POOL"] = "0"
-        off = XceptionEngine(xparams, max_batch=2)
-        off.apply_tuning({"block2_sepconv2": [0, 204]})
-        os.environ["KDL_SEP_POOL"] = "1"
-        on = XceptionEngine(xparams, max_batch=2)
-    finally:
-        if old is None:
-            os.environ.pop("KDL_SEP_POOL", None)
-        else:
-            os.environ["KDL_SEP_POOL"] = old
-    assert any(s.kind == "seppool" for s in on.steps) and not any(s.kind == "seppool" for s in off.steps)
-    assert off.tuning()["block2_sepconv2"] == [0, 204]
-    on.apply_tuning({k: v for k, v in off.tuning().items() if k != "block2_sepconv2"})
-    gen = torch.Generator().manual_seed(5)
-    img = torch.randint(0, 256, (2, 299, 299, 3), generator=gen, dtype=torch.uint8).cuda()
-    assert torch.equal(on.forward(img), off.forward(img))
-
-
-@pytest.mark.parametrize("batch,cfg", [(2, 143), (24, 143), (24, 146)])
-def test_xception_chained_middle_flow_is_bit_identical(xparams, batch, cfg):
-    """KDL_CHAIN: the middle flow's 24 separable convs as ONE ticketed launch (write-through
-    stores, per-(layer, M tile) counters, agent acquire) give exactly the activations and logits
-    of 24 separate launches of the same ws tile -- every layer, every element; no dependency
-    wait gave up. Batch 24: 91 M tiles per layer, so tiles of consecutive layers overlap."""
-    from kdl.engine.xception import XceptionEngine
-    e = XceptionEngine(xparams, max_batch=batch)
-    mids = [s for s in e.steps if s.kind == "conv" and s.name.startswith(tuple(f"block{i}_" for i in range(5, 13)))]
-    assert len(mids) == 24 and all(cfg in s.layer.candidates for s in mids)
-    e.apply_tuning({s.name: [0, cfg] for s in mids})
-    gen = torch.Generator().manual_seed(11)
-    img = torch.randint(0, 256, (batch, 299, 299, 3), generator=gen, dtype=torch.uint8).cuda()
-    ref = e.forward(img)
-    ref_act = {s.dst: e.bufs[s.dst].clone() for s in mids}
-    for s in mids:
-        e.bufs[s.dst].fill_(7.0)       # stale data would show
-    e.chain_cfg = cfg
-    e.invalidate()
-    names = e.program(batch).op_names()
-    chains = [n for n in names if n.startswith("chain[")]
-    assert len(chains) == 1 and not any(n == s.name for s in mids for n in names)
-    (sync,) = e._chain_sync.values()
-    for _ in range(3):                  # replays: the launch re-zeroes tickets and counters itself
-        sync.fill_(99)
-        got = e.forward(img)
-        torch.cuda.synchronize()
-        assert torch.equal(got, ref)
-        for s in mids:
-            assert torch.equal(e.bufs[s.dst], ref_act[s.dst]), s.name
-    assert int(sync[1]) == 0, "a dependency wait hit its spin limit (1) or tickets were stale (2)"
-    d = e.chain_layer_args(mids, batch)
-    assert int(sync[0]) == 24 * d["nM"] * d["nN"]      # every ticket taken exactly once
-
-
-def test_xception_chained_stage_pipeline_matches(xparams):
-    """Stage-pipelined bench configuration with chains: each stage's part of the middle flow is
-    one chained launch (7 + 17 layers), and the logits equal the unchained pipeline's."""
-    from kdl.engine.stages import StagePipe
-    from kdl.engine.xception import XceptionEngine
-    from kdl.engine import registry
-    B = 16
-    e = XceptionEngine(xparams, max_batch=B)
-    mids = [s for s in e.steps if s.kind == "conv" and s.name.startswith(tuple(f"block{i}_" for i in range(5, 13)))]
-    e.apply_tuning({s.name: [0, 143] for s in mids})
-    gen = torch.Generator().manual_seed(12)
-    imgs = [torch.randint(0, 256, (B, 299, 299, 3), generator=gen, dtype=torch.uint8).cuda() for _ in range(3)]
-    outs = {}
-    for chain in (0, 143):
-        e.chain_cfg = chain
-        e.invalidate()
-        sp = StagePipe(e, registry.get("xception").stage_cut)
-        outs[chain] = [sp.forward(x).clone() for x in imgs]
-        if chain:
-            names = [n for p in sp.program(B)[0] for n in p.op_names()]   # parity 0, every stage
-            assert sum(n.startswith("chain[") for n in names) == 2
-    for a, b in zip(outs[0], outs[143]):
-        assert torch.equal(a, b)

@@ -92,7 +92,7 @@ def test_cu_masks_are_disjoint_and_cover():
     assert sum(bin(x).count("1") for x in a + b) == 256
 
 
-def _xception_engine(fuse=False, chain=0):
+def _xception_engine():
     from kdl.engine import xception as XE
     from kdl.models import xception as X
 
@@ -101,9 +101,6 @@ def _xception_engine(fuse=False, chain=0):
             self.device = torch.device("cpu")
             self.max_batch, self.buckets, self.steps, self.in_kind = 1, [1], [], "u8"
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
-            self.branches, self.poolfuse = 0, fuse
-            self.seppool, self.seppool_cfg, self.chain_cfg, self._chain_sync = not fuse, 0, chain, {}
-            self.chain_min = 2
 
     p = X.init_params(seed=0)
     e = Fake(p)
@@ -111,35 +108,8 @@ def _xception_engine(fuse=False, chain=0):
     return e
 
 
-def _xception_steps(fuse=False):
-    return _xception_engine(fuse).steps
-
-
-def _runs(e, steps):
-    out, i = [], 0
-    while i < len(steps):
-        j = e._chain_end(steps, i)
-        if j - i >= 2:
-            out.append((steps[i].name, steps[j - 1].name, j - i))
-        i = max(j, i + 1)
-    return out
-
-
-def test_xception_chain_groups_the_middle_flow_within_each_stage():
-    from kdl.engine import registry
-    e = _xception_engine(chain=143)
-    # whole forward: the 24 separable convs of blocks 5-12 in one launch (block13's residual
-    # conv step comes before block13_sepconv1)
-    assert _runs(e, e.steps) == [("block5_sepconv1", "block12_sepconv3", 24)]
-    # stage-pipelined: the chain never crosses the stage cut
-    sp = _analyse(e.steps, registry.get("xception").stage_cut, scratch=["__dwtmp"])
-    got = [_runs(e, e.steps[lo:hi]) for lo, hi in sp.ranges]
-    assert got == [[("block5_sepconv1", "block7_sepconv1", 7)], [("block7_sepconv2", "block12_sepconv3", 17)]]
-    # off, or a tile whose halo does not stay within neighbouring M tiles: no chains
-    assert _runs(_xception_engine(chain=0), e.steps) == []
-    # a split (dw3x3 + GEMM) layer is not chained: it ends one run and starts none
-    e.steps[e.steps.index(next(s for s in e.steps if s.name == "block9_sepconv2"))].layer.split = True
-    assert [r[2] for r in _runs(e, e.steps)] == [13, 10]
+def _xception_steps():
+    return _xception_engine().steps
 
 
 def test_xception_default_cut_boundaries():
@@ -172,17 +142,3 @@ def test_resnet_cut_inside_stage_privatises_shared_buffers():
     # the default: three stages (cuts after layer2.1 and layer3.3), two parity-buffered boundaries
     sp3 = _analyse(e.steps, registry.get("resnet50").stage_cut)
     assert len(sp3.ranges) == 3 and sorted(sp3.boundary) == ["out14x1024_1", "out28x512_1"]
-
-
-def test_xception_residual_conv_carries_the_pool():
-    """KDL_POOLFUSE=1: entry/exit blocks lower to residual conv + max-pool as ONE 'convpool' step that reads
-    the block input (src) and the main branch (res) and writes the block output."""
-    steps = _xception_steps(fuse=True)
-    assert not [s for s in steps if s.kind == "pool"]
-    cp = [s for s in steps if s.kind == "convpool"]
-    assert [s.dst for s in cp] == ["block2_out", "block3_out", "block4_out", "block13_out"]
-    assert [s.res for s in cp] == ["block2_sepconv2_out", "block3_sepconv2_out", "block4_sepconv2_out",
-                                   "block13_sepconv2_out"]
-    idx = {s.name: i for i, s in enumerate(steps)}
-    for s in cp:                                  # after the main branch it pools
-        assert idx[s.name] > idx[s.res.replace("_out", "")]
