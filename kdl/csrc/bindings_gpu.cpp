@@ -152,6 +152,19 @@ GemmF8Args f8_args(const py::dict& d) {
   a.krot = I(d, "krot");
   return a;
 }
+EntryBlockArgs eb_args(const py::dict& d) {
+  EntryBlockArgs a{};
+  a.x = P<const uint16_t>(d, "x"); a.y = P<uint16_t>(d, "y");
+  a.w1 = P<const uint16_t>(d, "w1"); a.b1 = P<const float>(d, "b1"); a.dw1 = P<const float>(d, "dw1");
+  a.w2 = P<const uint16_t>(d, "w2"); a.b2 = P<const float>(d, "b2"); a.dw2 = P<const float>(d, "dw2");
+  a.wr = P<const uint16_t>(d, "wr"); a.br = P<const float>(d, "br");
+  a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
+  a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.grid = I(d, "grid");
+  a.steps = P<const int4>(d, "steps"); a.step_off = P<const int>(d, "step_off");
+  if (!a.x || !a.y || !a.w1 || !a.b1 || !a.dw1 || !a.w2 || !a.b2 || !a.dw2 || !a.wr || !a.br)
+    throw std::invalid_argument("entry_block: null pointer");
+  return a;
+}
 BlasLtArgs blaslt_args(const py::dict& d) {
   BlasLtArgs a{};
   a.x = P<const void>(d, "x"); a.w = P<const void>(d, "w"); a.y = P<void>(d, "y");
@@ -319,6 +332,16 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     chk(weight_scale(a, S(s)), "weight_scale");
   });
+  m.def("entry_block", [](int cfg, py::dict d, uintptr_t s) {
+    const auto a = eb_args(d);
+    py::gil_scoped_release nogil;
+    chk(entry_block(cfg, a, S(s)), "entry_block");
+  });
+  m.def("entry_block_config", [](int cfg) {
+    int c0 = 0, c1 = 0, pc = 0, lds = 0;
+    if (entry_block_config(cfg, &c0, &c1, &pc, &lds) != 0) throw std::out_of_range("bad entry_block config");
+    return py::make_tuple(c0, c1, pc, lds);
+  });
   m.def("gemm_f8", [](int cfg, py::dict d, uintptr_t s) {
     const auto a = f8_args(d);
     py::gil_scoped_release nogil;
@@ -435,6 +458,9 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_chscale", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_CHSCALE; op.name = name; op.cs = chs_args(d); p.add(op);
+      })
+      .def("add_entry_block", [](Program& p, const std::string& name, int cfg, py::dict d) {
+        Op op; op.kind = OP_ENTRY_BLOCK; op.name = name; op.cfg = cfg; op.eb = eb_args(d); p.add(op);
       })
       .def("add_gemm_f8", [](Program& p, const std::string& name, int cfg, py::dict d) {
         Op op; op.kind = OP_GEMM_F8; op.name = name; op.cfg = cfg; op.f8 = f8_args(d); p.add(op);

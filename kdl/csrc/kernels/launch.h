@@ -64,6 +64,29 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& a, hipStream_t s);
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads);
 int sepconv_ws_fits(int cfg, int W);
 
+// A whole Xception entry block (SeparableConv -> ReLU -> SeparableConv -> 3x3/2 max-pool, plus
+// the 1x1/2 residual conv) in one persistent launch, entry_block.hip. Workgroup g runs the
+// host-built steps [step_off[g], step_off[g+1]) of `steps`: int4 {image, strip, pooled row k,
+// mode} with mode 0 = warm-up (y1 only), 1 = warm-up (y1 + y2, no output), 2 = output row k.
+struct EntryBlockArgs {
+  const uint16_t* x;      // block input [B][H][W][ldx] bf16
+  uint16_t* y;            // block output [B][OH][OW][ldy] bf16
+  const uint16_t* w1;     // sepconv1 pointwise, packed [C1/16][C0/32][64][8] (BN scale folded)
+  const float* b1;        // [C1] BN shift
+  const float* dw1;       // sepconv1 depthwise [9][C0] fp32
+  const uint16_t* w2;     // sepconv2 pointwise, packed [C1/16][C1/32][64][8]
+  const float* b2;
+  const float* dw2;       // [9][C1]
+  const uint16_t* wr;     // residual 1x1/2 conv, packed [C1/16][C0/32][64][8]
+  const float* br;
+  int B, H, W, OH, OW, ldx, ldy;
+  int grid;               // workgroups (= len(step_off) - 1)
+  const int4* steps;
+  const int* step_off;
+};
+hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s);
+int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds);
+
 // cfg >= C3_CFG_BASE: 3x3 'valid' conv over 2-D tiles with an LDS halo patch (MODE_CONV, cin 32 only,
 // conv3x3_2d.hip: Xception block1_conv2).
 constexpr int C3_CFG_BASE = 208;

@@ -7,6 +7,8 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
     conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
     conv_gemm MODE_PW    residual 1x1/2 convs + BN
     pool_add             TF-'same' 3x3/2 max-pool + residual add
+    entry_block          KDL_ENTRY_BLOCK=1: block2 (both separable convs, the pool and the
+                         residual conv) as ONE persistent launch (kdl/ops/entry_block.py)
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
 
 = 41 launches per forward (vs ~168 unfused TF ops), captured into
@@ -39,6 +41,9 @@ class XceptionEngine(EngineBase):
         super().__init__(device, max_batch, buckets)
         self.in_kind = in_kind
         self.head = head
+        # fused entry blocks (entry_block.hip): block numbers lowered to one launch each
+        eb = os.environ.get("KDL_ENTRY_BLOCK", "0")
+        self.fused_blocks = {2} if eb == "1" else {int(v) for v in eb.split(",") if v.strip() and v != "0"}
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
@@ -85,11 +90,20 @@ class XceptionEngine(EngineBase):
                 oh = (H - 1) // 2 + 1
                 rname = f"{rc.name}_out"
                 lay = self._pw(p, rc, dev)
+                _, pt, _ = tf_same_pad(H, 3, 2)
+                out = f"block{bi + 1}_out"
+                if bi + 1 in self.fused_blocks:
+                    from ..ops.entry_block import EntryBlock
+                    s1, s2 = (self._sep(p, op, dev) for op in blk.main)
+                    fb = EntryBlock(f"block{bi + 1}", s1, s2, lay, device=dev)
+                    self.steps.append(Step("block", f"block{bi + 1}", src=cur, dst=out, geom=(H, H, oh, oh),
+                                           extra=dict(eb=fb)))
+                    self.shapes[out] = (oh, oh, s2.ldy)
+                    cur, H = out, oh
+                    continue
                 self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh)))
                 self.shapes[rname] = (oh, oh, lay.ldy)
                 y = cur
-                _, pt, _ = tf_same_pad(H, 3, 2)
-                out = f"block{bi + 1}_out"
                 for op in blk.main:
                     lay = self._sep(p, op, dev)
                     dst = f"{op.name}_out"
@@ -213,6 +227,8 @@ class XceptionEngine(EngineBase):
                                               y=self._ptr(step.dst), B=b, H=H, W=W, OH=OH, OW=OW,
                                               C=step.extra["C"], pad_top=step.extra["pad"],
                                               pad_left=step.extra["pad"]))
+        elif step.kind == "block":
+            step.extra["eb"].emit(prog, self._ptr(step.src), self._ptr(step.dst), b, H, W)
         elif step.kind == "head":
             hd = self.head
             prog.add_head(step.name, dict(x=self._ptr(step.src), w1=_lib.ptr(self.w1),

@@ -70,3 +70,11 @@ def stream_ptr(stream: torch.cuda.Stream | None = None) -> int:
 
 def ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else int(t.data_ptr())
+
+
+def num_cus(device: torch.device | str | None = None) -> int:
+    """Compute units of a GPU (persistent kernels launch one workgroup per CU); 256 on MI355X."""
+    d = torch.device(device) if device is not None else torch.device("cuda")
+    if d.type != "cuda" or not torch.cuda.is_available():
+        return 256
+    return torch.cuda.get_device_properties(d).multi_processor_count

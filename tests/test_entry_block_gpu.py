@@ -1,0 +1,90 @@
+"""Fused Xception entry block (entry_block.hip, kdl/ops/entry_block.py) against the fp32
+Keras-semantics oracle of the same block (SepConv -> ReLU -> SepConv -> 3x3/2 'same' max-pool +
+BN(1x1/2 conv)), and the engine lowering (KDL_ENTRY_BLOCK) against the whole-network oracle.
+Graph reference: /root/reference/guide.md:222-229 (the served Xception's I/O contract)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from kdl.models import xception as X
+from kdl.models.layers import maxpool_same
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _block_oracle(p, x_nhwc, blk):
+    """fp32 forward of entry block ``blk`` of X.SPEC on an NHWC input."""
+    x = x_nhwc.float().permute(0, 3, 1, 2)
+    b = X.SPEC[blk - 1]
+    res = X._bn(X._conv(x, p, b.res_conv), p, b.res_conv.bn, False)
+    y = x
+    for op in b.main:
+        y = X._bn(X._sep(torch.relu(y) if op.relu_in else y, p, op), p, op.bn, False)
+        if op.relu_out:
+            y = torch.relu(y)
+    return (maxpool_same(y, 3, 2) + res).permute(0, 2, 3, 1)
+
+
+def _layers(p, blk):
+    from kdl.engine.xception import XceptionEngine as XE
+    b = X.SPEC[blk - 1]
+    return XE._sep(p, b.main[0], DEV), XE._sep(p, b.main[1], DEV), XE._pw(p, b.res_conv, DEV)
+
+
+@pytest.mark.parametrize("B,grid", [(2, None), (2, 5), (3, 97), (1, 1)])
+def test_entry_block2_matches_oracle(xparams, B, grid):
+    from kdl.ops.entry_block import EntryBlock
+    s1, s2, r = _layers(xparams, 2)
+    eb = EntryBlock("block2", s1, s2, r, device=DEV, grid=grid)
+    gen = torch.Generator().manual_seed(21 + B)
+    # block1_conv2 output: post-ReLU, O(1)
+    x = torch.relu(torch.randn(B, 147, 147, 64, generator=gen)).to(torch.bfloat16)
+    ref = _block_oracle(xparams, x.float(), 2)
+    y = torch.full((B, 74, 74, 128), float("nan"), dtype=torch.bfloat16, device=DEV)
+    eb.emit(None, x.to(DEV).data_ptr(), y.data_ptr(), B, 147, 147)
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert torch.isfinite(got).all()
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    print(f"entry block2 B={B} grid={grid}: rel max err {err:.2e}")
+    assert err < 2e-2, err
+
+
+def test_entry_block2_replays_bit_identical(xparams):
+    """Persistent kernel, host step table: two launches give identical bytes."""
+    from kdl.ops.entry_block import EntryBlock
+    s1, s2, r = _layers(xparams, 2)
+    eb = EntryBlock("block2", s1, s2, r, device=DEV)
+    gen = torch.Generator().manual_seed(5)
+    x = torch.relu(torch.randn(4, 147, 147, 64, generator=gen)).to(torch.bfloat16).to(DEV)
+    y1 = torch.empty((4, 74, 74, 128), dtype=torch.bfloat16, device=DEV)
+    y2 = torch.empty_like(y1)
+    eb.emit(None, x.data_ptr(), y1.data_ptr(), 4, 147, 147)
+    eb.emit(None, x.data_ptr(), y2.data_ptr(), 4, 147, 147)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+
+
+def test_engine_with_fused_block2_matches_oracle(xparams):
+    from kdl.engine.xception import XceptionEngine
+    old = os.environ.get("KDL_ENTRY_BLOCK")
+    os.environ["KDL_ENTRY_BLOCK"] = "1"
+    try:
+        eng = XceptionEngine(xparams, max_batch=4, buckets=[1, 4])
+    finally:
+        if old is None:
+            os.environ.pop("KDL_ENTRY_BLOCK")
+        else:
+            os.environ["KDL_ENTRY_BLOCK"] = old
+    assert any(s.kind == "block" for s in eng.steps)
+    gen = torch.Generator().manual_seed(11)
+    img = torch.randint(0, 256, (3, 299, 299, 3), generator=gen, dtype=torch.uint8)
+    ref = X.xception_forward(xparams, img.float() / 127.5 - 1.0)
+    out = eng.forward(img.cuda()).cpu()
+    err = ((out - ref).abs().max() / ref.abs().max()).item()
+    print(f"engine with fused block2: logits rel err {err:.2e}")
+    assert err < 0.05, (out, ref)
+    assert torch.equal(eng.forward(img.cuda(), capture=True).cpu(), eng.forward(img.cuda(), capture=False).cpu())

@@ -92,7 +92,7 @@ def test_cu_masks_are_disjoint_and_cover():
     assert sum(bin(x).count("1") for x in a + b) == 256
 
 
-def _xception_engine():
+def _xception_engine(fused=()):
     from kdl.engine import xception as XE
     from kdl.models import xception as X
 
@@ -101,6 +101,7 @@ def _xception_engine():
             self.device = torch.device("cpu")
             self.max_batch, self.buckets, self.steps, self.in_kind = 1, [1], [], "u8"
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
+            self.fused_blocks = set(fused)
 
     p = X.init_params(seed=0)
     e = Fake(p)
@@ -142,3 +143,38 @@ def test_resnet_cut_inside_stage_privatises_shared_buffers():
     # the default: three stages (cuts after layer2.1 and layer3.3), two parity-buffered boundaries
     sp3 = _analyse(e.steps, registry.get("resnet50").stage_cut)
     assert len(sp3.ranges) == 3 and sorted(sp3.boundary) == ["out14x1024_1", "out28x512_1"]
+
+
+def test_xception_fused_entry_block_lowering():
+    """KDL_ENTRY_BLOCK: block2's residual conv, both separable convs and the pool become ONE
+    'block' step reading the block input and writing the block output; the stage cut analysis
+    is unchanged (the cut is in the middle flow)."""
+    from kdl.engine import registry
+    base = _xception_engine()
+    e = _xception_engine(fused=[2])
+    names = [s.name for s in e.steps]
+    assert "block2" in names and not {"conv2d", "block2_sepconv1", "block2_sepconv2", "block2_pool"} & set(names)
+    st = e.steps[names.index("block2")]
+    assert st.kind == "block" and st.src == "stem2" and st.dst == "block2_out" and st.geom == (147, 147, 74, 74)
+    assert len(e.steps) == len(base.steps) - 3
+    assert e.shapes["block2_out"] == base.shapes["block2_out"]
+    sp = _analyse(e.steps, registry.get("xception").stage_cut, scratch=["__dwtmp"])
+    assert sp.boundary == ["block6_sepconv3_out", "block7_sepconv1_out"]
+
+
+def test_entry_block_plan_covers_every_row_once():
+    from kdl.ops.entry_block import OUT, WARM_Y1, WARM_Y2, plan_steps
+    for B, grid in ((2, 7), (32, 256), (1, 1), (3, 1000)):
+        steps, off = plan_steps(B, 74, 74, 15, grid)
+        assert off[0] == 0 and off[-1] == len(steps) and all(a <= b for a, b in zip(off, off[1:]))
+        outs = [(b, s, k) for b, s, k, m in steps if m == OUT]
+        assert sorted(outs) == [(b, s, k) for b in range(B) for s in range(5) for k in range(74)]
+        per_wg = [sum(1 for st in steps[off[g]:off[g + 1]] if st[3] == OUT) for g in range(len(off) - 1)]
+        assert max(per_wg) - min(per_wg) <= 1                      # balanced
+        for g in range(len(off) - 1):                              # every run starts with its warm-ups
+            run = steps[off[g]:off[g + 1]]
+            for i, (b, s, k, m) in enumerate(run):
+                if m == OUT and (i < 2 or run[i - 1][:2] != (b, s) or run[i - 1][3] == WARM_Y1):
+                    raise AssertionError((g, i))
+                if m == WARM_Y1:
+                    assert run[i + 1] == (b, s, k + 1, WARM_Y2) and run[i + 2][2:] == (k + 2, OUT)
