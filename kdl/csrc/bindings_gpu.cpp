@@ -7,6 +7,7 @@
 
 #include "kernels/launch.h"
 #include "runtime/engine.h"
+#include "runtime/comm.h"
 #include "runtime/hip_backend.h"
 
 namespace py = pybind11;
@@ -407,6 +408,58 @@ PYBIND11_MODULE(_C, m) {
           throw std::runtime_error("HipExecBackend: batch failed");
         return std::make_tuple(reinterpret_cast<uintptr_t>(out), t.h2d_ms, t.forward_ms, t.d2h_ms);
       });
+
+  // ---- RCCL data-parallel serving (runtime/comm.h)
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes id, int nranks, int rank, int device) {
+             const std::string s = id;
+             py::gil_scoped_release nogil;       // every rank blocks here until all have joined
+             return new RcclComm(s, nranks, rank, device);
+           }),
+           py::arg("id"), py::arg("nranks"), py::arg("rank"), py::arg("device"))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def("abort", &RcclComm::abort)
+      .def("async_error", &RcclComm::async_error);
+  py::class_<DpLeader>(m, "DpLeader")
+      .def(py::init([](HipExecBackend* local, RcclComm* sc, RcclComm* ga, std::vector<int> buckets, double timeout_s) {
+             return new DpLeader(local, sc, ga, std::move(buckets), timeout_s);
+           }),
+           py::arg("local"), py::arg("scatter"), py::arg("gather"), py::arg("rank_buckets"), py::arg("timeout_s") = 120.0,
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def("api_ptr", [](const DpLeader& l) { return reinterpret_cast<uintptr_t>(l.api()); })
+      .def_property_readonly("world", &DpLeader::world)
+      .def_property_readonly("steps", &DpLeader::steps)
+      .def("send_ctrl", [](DpLeader& l, int cmd, int version) {
+        py::gil_scoped_release nogil;
+        return l.send_ctrl(cmd, version);
+      })
+      // direct use without the executor (tests / bench): issue + complete of one slot
+      .def("run", [](DpLeader& l, int slot, int bucket, int n_real) {
+        py::gil_scoped_release nogil;
+        const float* out = nullptr;
+        kdl_device_times t{};
+        if (l.issue(slot, bucket, n_real) != 0 || l.complete(slot, &out, &t) != 0)
+          throw std::runtime_error("DpLeader: step failed");
+        return reinterpret_cast<uintptr_t>(out);
+      });
+  py::class_<DpFollower>(m, "DpFollower")
+      .def(py::init([](HipExecBackend* local, RcclComm* sc, RcclComm* ga) { return new DpFollower(local, sc, ga); }),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def_property_readonly("steps", &DpFollower::steps)
+      // serve until a non-batch control word; returns (cmd, version, seq)
+      .def("run", [](DpFollower& f) {
+        DpCtrl c{};
+        {
+          py::gil_scoped_release nogil;
+          c = f.run();
+        }
+        return std::make_tuple(c.cmd, c.version, c.seq);
+      });
+  m.attr("DP_STOP") = int(DP_STOP);
+  m.attr("DP_BATCH") = int(DP_BATCH);
+  m.attr("DP_RELOAD") = int(DP_RELOAD);
 
   py::class_<Program>(m, "Program")
       .def(py::init<>())

@@ -10,6 +10,7 @@
 #include <sstream>
 
 #include "runtime/batcher.h"
+#include "runtime/dp_schedule.h"
 #include "runtime/executor.h"
 #include "runtime/sstable.h"
 #include "runtime/tfproto.h"
@@ -35,6 +36,22 @@ PYBIND11_MODULE(_rt, m) {
   m.def("now_us", &now_us);
 
   py::register_exception<ProtoError>(m, "ProtoError", PyExc_ValueError);
+
+  // data-parallel message schedule (runtime/dp_schedule.h): the exact per-rank op lists the
+  // RCCL backend posts, exposed so a CPU test can match every rank's sends against its peers'
+  auto msgs_py = [](const std::vector<DpMsg>& v) {
+    py::list out;
+    for (const auto& m : v) out.append(py::make_tuple(m.channel, m.send, m.peer, m.bytes, m.what, m.group));
+    return out;
+  };
+  m.def("dp_leader_step", [msgs_py](int world, size_t item_bytes, int out_cols, int cmd, int shard) {
+    return msgs_py(dp_leader_step(DpGeometry{world, item_bytes, out_cols}, cmd, shard));
+  });
+  m.def("dp_follower_step", [msgs_py](int world, size_t item_bytes, int out_cols, int cmd, int shard, bool next) {
+    return msgs_py(dp_follower_step(DpGeometry{world, item_bytes, out_cols}, cmd, shard, next));
+  });
+  m.def("dp_plan_shard", &dp_plan_shard);
+  m.attr("DP_CTRL_BYTES") = int(sizeof(DpCtrl));
 
   m.def("parse_predict_request", [](py::bytes req) {
     std::string_view sv = req;  // zero-copy view of the Python bytes

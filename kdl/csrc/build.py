@@ -44,6 +44,7 @@ def _hipcc() -> str:
 GPU_SOURCES = sorted((HERE / "kernels").glob("*.hip")) + [HERE / "runtime" / "engine.cpp",
                                                          HERE / "runtime" / "blaslt.cpp",
                                                          HERE / "runtime" / "hip_backend.cpp",
+                                                         HERE / "runtime" / "comm.cpp",
                                                          HERE / "bindings_gpu.cpp"]
 RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp")] + [
     HERE / "bindings_rt.cpp"]
@@ -89,9 +90,10 @@ def build_gpu(force: bool = False, njobs: int = 8, verbose: bool = True) -> Path
     _compile_all(jobs, njobs)
     if force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         # hipBLASLt (the vendor GEMM node, runtime/blaslt.cpp): SONAME libhipblaslt.so.1, the same
-        # as the copy torch loads first (import torch precedes kdl._C), so one instance is shared
+        # as the copy torch loads first (import torch precedes kdl._C), so one instance is shared;
+        # the same holds for RCCL (runtime/comm.cpp, SONAME librccl.so.1)
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-L/opt/rocm/lib",
-              "-lhipblaslt", "-o", str(out)])
+              "-lhipblaslt", "-lrccl", "-o", str(out)])
         if verbose:
             print(f"[kdl.build] linked {out.relative_to(ROOT)}", flush=True)
     return out

@@ -100,6 +100,39 @@ void HipExecBackend::add_recipe(int bucket, const std::vector<hipStream_t>& stre
   recipes_.emplace(bucket, std::move(r));
 }
 
+int HipExecBackend::launch(int slot, int bucket, hipEvent_t ready, hipStream_t* last) {
+  if (slot < 0 || slot >= nslots_) return -1;
+  auto it = recipes_.find(bucket);
+  if (it == recipes_.end()) return -1;
+  Recipe& r = it->second;
+  const int p = int(r.issued & 1);
+  ++r.issued;
+  for (int k = 0; k < r.K; ++k) {
+    hipStream_t st = r.streams[k];
+    KDL_TRY(hipStreamWaitEvent(st, k == 0 ? ready : r.done[p][k - 1], 0));
+    if (r.wait_for[k] > k) KDL_TRY(hipStreamWaitEvent(st, r.done[p][r.wait_for[k]], 0));
+    if (k == 0 && timing_) KDL_TRY(hipEventRecord(ev_fw0_[slot], st));
+    try {
+      r.progs[slot][p][k]->launch(st);
+    } catch (const std::exception&) {
+      return -1;
+    }
+    KDL_TRY(hipEventRecord(r.done[p][k], st));
+  }
+  *last = r.streams[r.K - 1];
+  return 0;
+}
+
+void* HipExecBackend::dev_in(int slot, int bucket) const {
+  auto it = recipes_.find(bucket);
+  return it == recipes_.end() || slot < 0 || slot >= nslots_ ? nullptr : it->second.dev_in[slot];
+}
+
+void* HipExecBackend::dev_out(int slot, int bucket) const {
+  auto it = recipes_.find(bucket);
+  return it == recipes_.end() || slot < 0 || slot >= nslots_ ? nullptr : it->second.dev_out[slot];
+}
+
 int HipExecBackend::issue(int slot, int bucket, int n_real) {
   (void)n_real;                               // padding rows are computed and ignored
   if (slot < 0 || slot >= nslots_) return -1;
@@ -110,21 +143,8 @@ int HipExecBackend::issue(int slot, int bucket, int n_real) {
   if (timing_) KDL_TRY(hipEventRecord(ev_h2d0_[slot], copy_));
   KDL_TRY(hipMemcpyAsync(r.dev_in[slot], staging_[slot], item_bytes_ * bucket, hipMemcpyHostToDevice, copy_));
   KDL_TRY(hipEventRecord(ev_h2d1_[slot], copy_));
-  const int p = int(r.issued & 1);
-  ++r.issued;
-  for (int k = 0; k < r.K; ++k) {
-    hipStream_t st = r.streams[k];
-    KDL_TRY(hipStreamWaitEvent(st, k == 0 ? ev_h2d1_[slot] : r.done[p][k - 1], 0));
-    if (r.wait_for[k] > k) KDL_TRY(hipStreamWaitEvent(st, r.done[p][r.wait_for[k]], 0));
-    if (k == 0 && timing_) KDL_TRY(hipEventRecord(ev_fw0_[slot], st));
-    try {
-      r.progs[slot][p][k]->launch(st);
-    } catch (const std::exception&) {
-      return -1;
-    }
-    KDL_TRY(hipEventRecord(r.done[p][k], st));
-  }
-  hipStream_t last = r.streams[r.K - 1];
+  hipStream_t last = nullptr;
+  if (launch(slot, bucket, ev_h2d1_[slot], &last) != 0) return -1;
   if (timing_) KDL_TRY(hipEventRecord(ev_fw1_[slot], last));
   KDL_TRY(hipMemcpyAsync(out_[slot], r.dev_out[slot], sizeof(float) * out_cols_ * bucket, hipMemcpyDeviceToHost, last));
   KDL_TRY(hipEventRecord(ev_done_[slot], last));

@@ -37,6 +37,19 @@ class HipExecBackend {
   uint8_t* staging(int slot) { return staging_[slot]; }
   const float* host_out(int slot) const { return out_[slot]; }
   int issue(int slot, int bucket, int n_real);
+  // the recipe of `bucket` alone (no copies): stage 0 waits `ready`; *last = the last stage's
+  // stream (its work is queued behind the forward). For the data-parallel ranks (comm.cpp).
+  int launch(int slot, int bucket, hipEvent_t ready, hipStream_t* last);
+  void* dev_in(int slot, int bucket) const;
+  void* dev_out(int slot, int bucket) const;
+  int device() const { return device_; }
+  int nslots() const { return nslots_; }
+  int max_batch() const { return max_batch_; }
+  size_t item_bytes() const { return item_bytes_; }
+  int out_cols() const { return out_cols_; }
+  hipStream_t copy_stream() const { return copy_; }
+  float* host_out_mut(int slot) { return out_[slot]; }
+  hipEvent_t done_event(int slot) const { return ev_done_[slot]; }
   int complete(int slot, const float** out, kdl_device_times* t);
 
  private:

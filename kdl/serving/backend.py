@@ -313,13 +313,21 @@ class GPUExecutor(_Executor):
     def healthy(self) -> bool:
         return self.native.healthy() if self.native is not None else self._healthy
 
+    def engine_buckets(self) -> list[int]:
+        """Batch sizes the local engine captures graphs for (data parallel: per-rank shards)."""
+        return self.runner.buckets
+
+    def staging_rows(self) -> int:
+        """Images per pinned staging slot (data parallel: the whole node's batch)."""
+        return self.engine_buckets()[-1]
+
     def setup(self):
         from ..engine import registry
         from ..engine.tuning import tuning_path
         torch.cuda.set_device(self.device)
         r = self.runner
         src = r.source
-        bs = r.buckets
+        bs = self.engine_buckets()
         fam = registry.variant(src.family, r.cfg.dtype)      # --dtype picks the engine variant
         cap = bool(self.engine_kwargs.get("graph", True))      # --graph off: eager launches
         in_kind = "u8" if r.sig.input_dtype == P.DT_UINT8 else "f32"
@@ -403,8 +411,8 @@ class GPUExecutor(_Executor):
         (pinned staging, H2D -> graphs -> D2H per slot, HIP-event stage times) driven by a
         kdl._rt.Executor C++ thread that pulls from the signature's batcher."""
         r, rt = self.runner, _lib.rt()
-        bs = r.buckets
-        be = self._rt.HipExecBackend(self.device, self.depth, item_bytes, bs[-1], classes,
+        bs = self.engine_buckets()
+        be = self._rt.HipExecBackend(self.device, self.depth, item_bytes, self.staging_rows(), classes,
                                      copy_stream=self.copy_stream.cuda_stream, timing=True)
         keep = []
         for bk in bs:
@@ -421,9 +429,15 @@ class GPUExecutor(_Executor):
                           [e.slot_logits(s).data_ptr() for s in range(self.depth)])
         self._native_keep = keep
         self.backend = be
+        if r.batcher is None:                 # a data-parallel follower: no batcher, no executor thread
+            return
         fail, delay_us = self.faults.native_args(self.name)
-        self.native = rt.Executor(r.batcher, be, r.exec_group, name=self.name, eager=self.eager,
+        self.native = rt.Executor(r.batcher, self.wrap_backend(be), r.exec_group, name=self.name, eager=self.eager,
                                   max_failures=self.max_failures, fail_batches=fail, delay_us=delay_us)
+
+    def wrap_backend(self, be):
+        """The device backend handed to the native executor (data parallel: rank 0's DpLeader)."""
+        return be
 
     def run_native(self) -> None:
         self.native.start()
@@ -579,9 +593,10 @@ class SignatureRunner:
         self.faults = FaultInjector()
         self.exec_group = _lib.rt().ExecGroup()     # native executors: last one out shuts the batcher
         if dp:
-            from .dp import make_executor_class
+            from .dp import make_executor_class, make_native_executor_class, native_ok
             dev = torch.device("cuda", devices[0]) if devices else torch.device("cpu")
-            self.executors.append(make_executor_class()(self, dev, cfg.dp_world))
+            cls = make_native_executor_class() if native_ok(cfg, dev) else make_executor_class()
+            self.executors.append(cls(self, dev, cfg.dp_world))
         elif devices:
             for d in devices:
                 for i in range(cfg.executors_for(len(devices))):

@@ -79,7 +79,7 @@ class ServerConfig:
     scatter: str = "host"
     dp_world: int = 0             # processes (GPUs) of the rccl group; 0 = every visible GPU
     dp_rank: int = -1             # set by the launcher
-    dp_signature: str = "serving_default"
+    dp_signature: str = "serving_uint8"
     log_format: str = "text"      # text | json (one JSON object per line, for log shippers)
     stats_log_interval_s: float = 0.0   # > 0: a "stats" log record (metrics snapshot) this often
 
@@ -152,7 +152,7 @@ def build_parser() -> argparse.ArgumentParser:
                          "process feeds its own GPU (see --procs)")
     ap.add_argument("--dp_world", type=int, default=0, help="GPUs of the --scatter rccl group (0 = all visible)")
     ap.add_argument("--dp_rank", type=int, default=-1, help=argparse.SUPPRESS)   # set by the rccl launcher
-    ap.add_argument("--dp_signature", default="serving_default",
+    ap.add_argument("--dp_signature", default="serving_uint8",
                     help="the signature served data parallel under --scatter rccl (others run on rank 0's GPU)")
     ap.add_argument("--log_format", choices=["text", "json"], default=None,
                     help="json: one JSON object per log line (env KDL_LOG_FORMAT)")

@@ -3,26 +3,31 @@
 The north star's serving topology: ONE server process
 (rank 0) owns the gRPC/REST front-end and the dynamic batcher; it forms batches of up
 to ``world x per-rank bucket`` images and runs them as one collective step with every
-other rank (one process per GPU, ``torch.distributed`` backend "nccl" = RCCL over
-xGMI; "gloo" on CPU):
+other rank (one process per GPU):
 
-    C1  broadcast_params   rank 0 read the model version from disk -> every rank, once
-    ctrl broadcast_ctrl    (n_real, per-rank shard, stop)
-    C2  scatter_batch      rank 0's uint8 / f32 batch (one H2D on GPU 0) -> each rank's
-                           shard, written straight into its engine's static input
-    C3  gather_logits      every rank's fp32 logits -> rank 0 -> D2H -> handlers
+    C1  share_source       rank 0 read the model version from disk -> every rank, once per
+                           version (torch.distributed broadcast of the flattened weights)
+    C2  scatter            rank 0's uint8 batch (268 KB/img; one pinned staging slot) -> each
+                           follower's shard, straight into its engine's static input slot
+    C3  gather             every follower's fp32 logits -> rank 0 -> D2H -> handlers
 
-(``kdl.parallel.dp``). The reference scales by Deployment replicas behind a Service
-(`tf-serving-clothing-model-deployment.yaml:8`); ``--procs N`` (one independent server
-per GPU on a shared port) is the other topology here and the default of the k8s
-manifest: rank 0's single Python front-end tops out near 29k img/s
-(``profiles/serve_closed_loop_r3.jsonl``, null device), below one node's GPUs, while
-``--procs`` has no such ceiling. This mode is the collective path for deployments that
-want one endpoint, one batcher and one model load.
+GPU (default): the NATIVE path (kdl/csrc/runtime/comm.cpp). Rank 0's C++ executor thread drives
+a ``DpLeader`` -- rank 0's own HipExecBackend (its shard goes H2D straight into its engine and
+its stage-pipelined graphs start at once) plus ncclSend / ncclRecv of a control word, the
+shards and the logits on two RCCL communicators -- with ``--exec_depth`` steps in flight.
+Followers run ``DpFollower.run()``: a C++ loop, GIL released, keyed by the received control
+word (per-rank bucket -> which captured graph), no Python per step. CPU / gloo: the
+torch.distributed reference implementation of the same protocol (``kdl.parallel.dp``).
 
-One signature (``--dp_signature``, default ``serving_default``) runs data parallel; the
-others are served by rank 0's own GPU. Version hot-reload is off in this mode (the
-followers build their engines once).
+Hot reload: when rank 0's model manager loads a new version, the new DP executor asks the
+current leader to send DP_RELOAD(version); followers leave their loop, receive the new weights
+(C1), rebuild, and join the new communicators. The DP signature is unavailable while the
+followers rebuild (rank 0's other signatures keep serving); the old version's executor fails
+its remaining batches (UNAVAILABLE to clients) until it is retired.
+
+The reference scales by Deployment replicas behind a Service
+(`tf-serving-clothing-model-deployment.yaml:8`); ``--procs N`` (one independent server per
+GPU on a shared port) is the other topology here.
 """
 from __future__ import annotations
 
@@ -126,6 +131,57 @@ def local_forward(source, sig, dev: torch.device, buckets: list[int]):
 
 
 # ---------------------------------------------------------------------- followers
+def native_ok(cfg, dev: torch.device) -> bool:
+    """The C++/RCCL path (comm.cpp) runs on GPUs unless KDL_DP_NATIVE=0."""
+    import os
+    return dev.type == "cuda" and os.environ.get("KDL_DP_NATIVE", "1") != "0"
+
+
+class _FollowerRunner:
+    """What a GPUExecutor reads from its SignatureRunner, for a follower (no batcher)."""
+
+    def __init__(self, source, sig, cfg):
+        from .backend import FaultInjector
+        self.source, self.sig, self.cfg = source, sig, cfg
+        self.buckets = cfg.rank_buckets()
+        self.batcher = None
+        self.exec_group = None
+        self.faults = FaultInjector("")
+
+
+def _comms(rank: int, world: int, device: int):
+    """Two RCCL communicators (scatter, gather) on fresh unique ids from rank 0."""
+    from ..ops import _lib
+    C = _lib.lib()
+    ids = [C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else [None, None]
+    dist.broadcast_object_list(ids, src=0)
+    return [C.RcclComm(i, world, rank, device) for i in ids]
+
+
+def follow_native(cfg, rank: int, world: int, dev: torch.device) -> int:
+    """A follower's life: per model version, receive the weights (C1), build the engine and
+    its graphs, join the version's communicators, then serve rank 0's steps in C++ until a
+    DP_STOP (exit) or DP_RELOAD (next version) control word."""
+    from ..ops import _lib
+    from .backend import GPUExecutor
+    C = _lib.lib()
+    while True:
+        source = share_source(None, dev)
+        sig = source.signatures[cfg.dp_signature]
+        ex = GPUExecutor(_FollowerRunner(source, sig, cfg), dev.index, cfg.engine_kwargs())
+        ex.setup()                      # engines, captured graphs, HipExecBackend recipes
+        comms = _comms(rank, world, dev.index)
+        f = C.DpFollower(ex.backend, *comms)
+        log.info("dp rank %d/%d on %s ready (native RCCL, %s, per-rank buckets %s)", rank, world, dev,
+                 cfg.dp_signature, cfg.rank_buckets())
+        cmd, version, seq = f.run()
+        log.info("dp rank %d: %s after %d steps", rank, "reload" if cmd == C.DP_RELOAD else "stop", f.steps)
+        del f, comms, ex
+        torch.cuda.synchronize(dev)
+        if cmd != C.DP_RELOAD:
+            return 0
+
+
 def follow(cfg, rank: int, world: int) -> int:
     """Ranks >= 1: receive the model (C1), build the DP signature's engine on this rank's
     GPU, then run rank 0's collective steps until it broadcasts stop. SIGTERM / SIGINT are
@@ -135,6 +191,10 @@ def follow(cfg, rank: int, world: int) -> int:
     for sg in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sg, signal.SIG_IGN)
     dev = init_group(cfg, rank, world)
+    if native_ok(cfg, dev):
+        rc = follow_native(cfg, rank, world, dev)
+        dist.destroy_process_group()
+        return rc
     source = share_source(None, dev)
     sig = source.signatures[cfg.dp_signature]
     buckets = cfg.rank_buckets()
@@ -149,6 +209,72 @@ def follow(cfg, rank: int, world: int) -> int:
 
 
 # ---------------------------------------------------------------------- rank 0 executor
+_ACTIVE = {"leader": None, "lock": None}
+
+
+def _active_lock():
+    import threading
+    if _ACTIVE["lock"] is None:
+        _ACTIVE["lock"] = threading.Lock()
+    return _ACTIVE["lock"]
+
+
+def make_native_executor_class():
+    from ..ops import _lib
+    from .backend import GPUExecutor
+
+    class DPNativeExecutor(GPUExecutor):
+        """Rank 0's executor of the data-parallel signature on the native path: the C++
+        executor thread issues each batch of world x shard images to a DpLeader (comm.cpp)."""
+
+        def __init__(self, runner, dev: torch.device, world: int, version: int | None = None):
+            super().__init__(runner, dev.index, runner.cfg.engine_kwargs())
+            self.name = f"dp{world}/{runner.sig.name}"
+            self.world, self.version = world, version
+            self.leader = None
+
+        def engine_buckets(self) -> list[int]:
+            return self.runner.cfg.rank_buckets()
+
+        def staging_rows(self) -> int:
+            return self.world * self.engine_buckets()[-1]
+
+        def setup(self):
+            import os
+            C = _lib.lib()
+            with _active_lock():
+                old = _ACTIVE["leader"]
+                if old is not None:          # a newer version: followers leave the old loop first
+                    old.send_ctrl(C.DP_RELOAD, int(self.version or 0))
+                    _ACTIVE["leader"] = None
+                # C1 for this version (the initial one was shared by server.main before loading)
+                if old is not None:
+                    share_source(self.runner.source, self.device_obj())
+                super().setup()              # engines, graphs, HipExecBackend; -> wrap_backend
+                self.timeout_s = float(os.environ.get("KDL_DP_TIMEOUT_S", "120"))
+                _ACTIVE["leader"] = self.leader
+
+        def device_obj(self) -> torch.device:
+            return torch.device("cuda", self.device)
+
+        def wrap_backend(self, be):
+            import os
+            self.comms = _comms(0, self.world, self.device)
+            self.leader = _lib.lib().DpLeader(be, *self.comms, self.engine_buckets(),
+                                              float(os.environ.get("KDL_DP_TIMEOUT_S", "120")))
+            return self.leader
+
+        def run_native(self) -> None:
+            try:
+                super().run_native()
+            finally:
+                with _active_lock():
+                    if _ACTIVE["leader"] is self.leader and self.leader is not None:
+                        self.leader.send_ctrl(_lib.lib().DP_STOP, 0)    # release the followers
+                        _ACTIVE["leader"] = None
+    return DPNativeExecutor
+
+
 def make_executor_class():
     from .backend import _Executor
 

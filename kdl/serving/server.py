@@ -168,11 +168,12 @@ def main(argv=None) -> int:
         if cfg.dp_rank > 0:
             return dp.follow(cfg, cfg.dp_rank, cfg.dp_world)
         # rank 0: the front-end. Load the model once, hand it to the group (C1), then serve
-        # with the dp signature's batcher feeding collective steps; no hot reload (the
-        # followers' engines are built once)
+        # with the dp signature's batcher feeding collective steps. Hot reload: native path
+        # only (the new version's DP executor re-runs C1 with the followers, serving/dp.py)
         dev = dp.init_group(cfg, 0, cfg.dp_world)
         cfg.gpu_index = dev.index if dev.type == "cuda" else -1
-        cfg.file_system_poll_wait_seconds = 0
+        if not dp.native_ok(cfg, dev):
+            cfg.file_system_poll_wait_seconds = 0
         if cfg.dp_signature not in cfg.warm_signatures:
             cfg.warm_signatures.append(cfg.dp_signature)
         from .model_repo import latest_version_source

@@ -251,11 +251,20 @@ def test_rccl_scatter_server_world1(tmp_path):
         u8 = rng.integers(0, 256, (3, 299, 299, 3), dtype=np.uint8)
         x = u8.astype(np.float32) / 127.5 - 1.0
         stub = PredictionStub(grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.max_send_message_length", -1)]))
+        ref = X.xception_forward(X.init_params(seed=0), torch.from_numpy(x)).numpy()
+        # the data-parallel signature (default serving_uint8): native DpLeader + RCCL comms
+        for n in (3, 8, 1):
+            r = stub.Predict(make_request(u8[:n] if n <= 3 else np.concatenate([u8] * 3)[:n],
+                                          signature="serving_uint8", input_key="images"), timeout=60)
+            got = np.asarray(r.outputs["dense_7"].float_val, np.float32).reshape(n, 10)
+            want = ref[:n] if n <= 3 else np.concatenate([ref] * 3)[:n]
+            assert np.abs(got - want).max() < 0.05 * np.abs(ref).max(), n
+        # the reference client's f32 serving_default request: rank 0's own executor
         r = stub.Predict(make_request(x), timeout=60)
         got = np.asarray(r.outputs["dense_7"].float_val, np.float32).reshape(3, 10)
-        ref = X.xception_forward(X.init_params(seed=0), torch.from_numpy(x)).numpy()
         assert np.abs(got - ref).max() < 0.05 * np.abs(ref).max()
-        assert "rccl data-parallel group of 1" in (tmp_path / "srv.log").read_text()
+        text = (tmp_path / "srv.log").read_text()
+        assert "rccl data-parallel group of 1" in text
     finally:
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGTERM)
@@ -264,3 +273,53 @@ def test_rccl_scatter_server_world1(tmp_path):
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
         logf.close()
+
+
+def test_native_dp_leader_world1_matches_local_backend(tmp_path):
+    """comm.cpp at world size 1 (one GPU on this box): two RCCL communicators, DpLeader wrapping
+    the same captured graphs as the single-GPU HipExecBackend; a batch through the leader gives
+    exactly the local backend's logits, and the stop control word goes out cleanly."""
+    import torch.distributed as dist
+
+    from kdl.engine.xception import XceptionEngine
+    from kdl.ops import _lib
+    C = _lib.lib()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        p = X.init_params(seed=0)
+        eng = XceptionEngine(p, max_batch=4, buckets=[2, 4])
+        eng.add_input_slots(2)
+        item = 299 * 299 * 3
+        be = C.HipExecBackend(0, 2, item, 4, 10)
+        progs = {b: [[[eng.program(b, True, s)]] * 2 for s in range(2)] for b in (2, 4)}
+        for b in (2, 4):
+            be.add_recipe(b, [eng.stream.cuda_stream], [0], progs[b], [eng.inputs[s].data_ptr() for s in range(2)],
+                          [eng.slot_logits(s).data_ptr() for s in range(2)])
+        ids = [C.rccl_unique_id(), C.rccl_unique_id()]
+        comms = [C.RcclComm(i, 1, 0, 0) for i in ids]
+        lead = C.DpLeader(be, *comms, [2, 4], 30.0)
+        rng = np.random.default_rng(3)
+        u8 = rng.integers(0, 256, (4, 299, 299, 3), dtype=np.uint8)
+        outs = []
+        for run in (be.run, lead.run):
+            st = np.frombuffer((ctypes_buffer(be.staging_ptr(0), 4 * item)), dtype=np.uint8)
+            st[:] = u8.reshape(-1)
+            res = run(0, 4, 4)
+            ptr = res[0] if isinstance(res, tuple) else res
+            outs.append(np.frombuffer(ctypes_buffer(ptr, 4 * 10 * 4), dtype=np.float32).copy().reshape(4, 10))
+        assert np.array_equal(outs[0], outs[1])
+        ref = X.xception_forward(p, torch.from_numpy(u8).float() / 127.5 - 1.0).numpy()
+        assert np.abs(outs[1] - ref).max() < 0.05 * np.abs(ref).max()
+        assert lead.send_ctrl(C.DP_STOP, 0) == 0 and lead.steps == 1
+        del lead, comms, be
+    finally:
+        dist.destroy_process_group()
+
+
+def ctypes_buffer(ptr: int, n: int):
+    import ctypes
+    return (ctypes.c_uint8 * n).from_address(ptr)
