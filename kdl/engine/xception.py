@@ -43,7 +43,7 @@ class XceptionEngine(EngineBase):
         self.head = head
         # fused entry blocks (entry_block.hip): block numbers lowered to one launch each
         eb = os.environ.get("KDL_ENTRY_BLOCK", "0")
-        self.fused_blocks = {2} if eb == "1" else {int(v) for v in eb.split(",") if v.strip() and v != "0"}
+        self.fused_blocks = {2, 3} if eb == "1" else {int(v) for v in eb.split(",") if v.strip() and v != "0"}
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)

@@ -28,6 +28,14 @@ def entry_block_config(cfg: int) -> tuple[int, int, int, int]:
     return tuple(_lib.lib().entry_block_config(cfg))
 
 
+# kernel config per (block input channels, block output channels): entry_block.hip KDL_EB_CONFIGS
+CONFIGS = {(64, 128): 0, (128, 256): 1}
+
+
+def supported(cin: int, cout: int) -> bool:
+    return (cin, cout) in CONFIGS
+
+
 def plan_steps(B: int, OH: int, OW: int, pc: int, grid: int) -> tuple[list[tuple[int, int, int, int]], list[int]]:
     """Step table + per-workgroup offsets. Work items (image, strip, pooled row) in row-major
     order are split into ``grid`` near-equal contiguous ranges; each maximal same-(image, strip)
@@ -55,16 +63,17 @@ def plan_steps(B: int, OH: int, OW: int, pc: int, grid: int) -> tuple[list[tuple
 class EntryBlock:
     """An entry block lowered to one entry_block launch (kernel config ``cfg``)."""
 
-    def __init__(self, name: str, sep1: ConvGemmLayer, sep2: ConvGemmLayer, res: ConvGemmLayer, cfg: int = 0,
+    def __init__(self, name: str, sep1: ConvGemmLayer, sep2: ConvGemmLayer, res: ConvGemmLayer, cfg: int | None = None,
                  device="cuda", grid: int | None = None):
-        """``grid``: workgroups (default: one per CU)."""
+        """``grid``: workgroups (default: one per CU); ``cfg``: kernel config (default: by channels)."""
+        cfg = CONFIGS[(sep1.cin_pad, sep1.n)] if cfg is None else cfg
         c0, c1, pc, lds = entry_block_config(cfg)
         assert sep1.mode == MODE_DW and sep2.mode == MODE_DW and res.mode == MODE_PW and res.stride == 2, name
         assert sep1.cin_pad == c0 and sep1.n == c1 and sep2.cin_pad == c1 and sep2.n == c1, (name, c0, c1)
         assert res.cin_pad == c0 and res.n == c1 and not sep2.relu_in and sep1.relu_out == 1 and sep2.relu_out == 0
         self.name, self.cfg, self.c0, self.c1, self.pc, self.lds = name, cfg, c0, c1, pc, lds
         self.relu_in = bool(sep1.relu_in)
-        assert not self.relu_in, "config 0 is block2 (no pre-activation on the block input)"
+        assert self.relu_in == (cfg == 1), "config 0 is block2 (no pre-activation), 1 is block3 (ReLU first)"
         self.sep1, self.sep2, self.res = sep1, sep2, res
         self.device = torch.device(device)
         self.grid = grid

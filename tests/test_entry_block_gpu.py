@@ -34,22 +34,30 @@ def _layers(p, blk):
     return XE._sep(p, b.main[0], DEV), XE._sep(p, b.main[1], DEV), XE._pw(p, b.res_conv, DEV)
 
 
-@pytest.mark.parametrize("B,grid", [(2, None), (2, 5), (3, 97), (1, 1)])
-def test_entry_block2_matches_oracle(xparams, B, grid):
+GEOM = {2: (147, 64, 74, 128), 3: (74, 128, 37, 256)}
+
+
+@pytest.mark.parametrize("blk,B,grid", [(2, 2, None), (2, 2, 5), (2, 3, 97), (2, 1, 1),
+                                        (3, 2, None), (3, 3, 7), (3, 1, 1)])
+def test_entry_block_matches_oracle(xparams, blk, B, grid):
+    """block2: 147 -> 74 (pool pad 1 on both sides); block3: 74 -> 37 (the asymmetric TF pad: 0
+    before, 1 after) with a ReLU on the block input before its first separable conv."""
     from kdl.ops.entry_block import EntryBlock
-    s1, s2, r = _layers(xparams, 2)
-    eb = EntryBlock("block2", s1, s2, r, device=DEV, grid=grid)
-    gen = torch.Generator().manual_seed(21 + B)
-    # block1_conv2 output: post-ReLU, O(1)
-    x = torch.relu(torch.randn(B, 147, 147, 64, generator=gen)).to(torch.bfloat16)
-    ref = _block_oracle(xparams, x.float(), 2)
-    y = torch.full((B, 74, 74, 128), float("nan"), dtype=torch.bfloat16, device=DEV)
-    eb.emit(None, x.to(DEV).data_ptr(), y.data_ptr(), B, 147, 147)
+    H, C0, OH, C1 = GEOM[blk]
+    s1, s2, r = _layers(xparams, blk)
+    eb = EntryBlock(f"block{blk}", s1, s2, r, device=DEV, grid=grid)
+    gen = torch.Generator().manual_seed(21 + B + blk)
+    # block2 input: block1_conv2 output (post-ReLU); block3 input: block2 output (signed)
+    x = torch.randn(B, H, H, C0, generator=gen)
+    x = (torch.relu(x) if blk == 2 else x).to(torch.bfloat16)
+    ref = _block_oracle(xparams, x.float(), blk)
+    y = torch.full((B, OH, OH, C1), float("nan"), dtype=torch.bfloat16, device=DEV)
+    eb.emit(None, x.to(DEV).data_ptr(), y.data_ptr(), B, H, H)
     torch.cuda.synchronize()
     got = y.float().cpu()
     assert torch.isfinite(got).all()
     err = ((got - ref).abs().max() / ref.abs().max()).item()
-    print(f"entry block2 B={B} grid={grid}: rel max err {err:.2e}")
+    print(f"entry block{blk} B={B} grid={grid}: rel max err {err:.2e}")
     assert err < 2e-2, err
 
 
@@ -71,7 +79,7 @@ def test_entry_block2_replays_bit_identical(xparams):
 def test_engine_with_fused_block2_matches_oracle(xparams):
     from kdl.engine.xception import XceptionEngine
     old = os.environ.get("KDL_ENTRY_BLOCK")
-    os.environ["KDL_ENTRY_BLOCK"] = "1"
+    os.environ["KDL_ENTRY_BLOCK"] = "2,3"
     try:
         eng = XceptionEngine(xparams, max_batch=4, buckets=[1, 4])
     finally:
@@ -79,12 +87,12 @@ def test_engine_with_fused_block2_matches_oracle(xparams):
             os.environ.pop("KDL_ENTRY_BLOCK")
         else:
             os.environ["KDL_ENTRY_BLOCK"] = old
-    assert any(s.kind == "block" for s in eng.steps)
+    assert [s.name for s in eng.steps if s.kind == "block"] == ["block2", "block3"]
     gen = torch.Generator().manual_seed(11)
     img = torch.randint(0, 256, (3, 299, 299, 3), generator=gen, dtype=torch.uint8)
     ref = X.xception_forward(xparams, img.float() / 127.5 - 1.0)
     out = eng.forward(img.cuda()).cpu()
     err = ((out - ref).abs().max() / ref.abs().max()).item()
-    print(f"engine with fused block2: logits rel err {err:.2e}")
+    print(f"engine with fused block2 + block3: logits rel err {err:.2e}")
     assert err < 0.05, (out, ref)
     assert torch.equal(eng.forward(img.cuda(), capture=True).cpu(), eng.forward(img.cuda(), capture=False).cpu())

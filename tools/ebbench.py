@@ -15,7 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--blocks", default="2")
+    ap.add_argument("--blocks", default="2,3")
     a = ap.parse_args()
     import torch
     from kdl.engine.tuning import tuning_path
