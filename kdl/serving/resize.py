@@ -25,44 +25,59 @@ IMAGE_SIGNATURE = "serving_image"
 MAX_PIXELS = int(os.environ.get("KDL_MAX_IMAGE_PIXELS", str(64 << 20)))   # per request, all images
 
 
+class _Ctx:
+    """One in-flight resize: its own stream and pinned / device buffers (grown on demand)."""
+
+    def __init__(self, dev: torch.device):
+        self.dev = dev
+        self.stream = torch.cuda.Stream(device=dev)
+        self.cap_in = self.cap_out = 0
+
+    def grow(self, n_in: int, n_out: int) -> None:
+        if n_in > self.cap_in:
+            self.cap_in = max(n_in, 2 * self.cap_in)
+            self.h_in = torch.empty(self.cap_in, dtype=torch.uint8).pin_memory()
+            self.d_in = torch.empty(self.cap_in, dtype=torch.uint8, device=self.dev)
+        if n_out > self.cap_out:
+            self.cap_out = max(n_out, 2 * self.cap_out)
+            self.h_out = torch.empty(self.cap_out, dtype=torch.uint8).pin_memory()
+            self.d_out = torch.empty(self.cap_out, dtype=torch.uint8, device=self.dev)
+
+
 class Resizer:
     """[n, H, W, 3] uint8 -> [n, S, S, 3] uint8, PIL-NEAREST exact. ``device``: a GPU index
-    (HIP kernel on a stream of its own) or None (numpy)."""
+    (HIP kernel) or None (numpy). Concurrent requests do not serialise: each call takes one of
+    up to ``KDL_RESIZE_CTX`` (default 4) contexts -- stream + pinned staging -- from a free list,
+    so the H2D, kernel and D2H of different requests overlap on the GPU."""
 
-    def __init__(self, size: int, device: int | None):
+    def __init__(self, size: int, device: int | None, contexts: int | None = None):
         self.S = size
         self.device = device
-        self._lock = threading.Lock()
+        self._tab_lock = threading.Lock()
         self._tabs: OrderedDict[tuple[int, int], tuple] = OrderedDict()
         if device is not None:
+            import queue
             self._dev = torch.device("cuda", device)
-            self.stream = torch.cuda.Stream(device=self._dev)
-            self._cap_in = self._cap_out = 0
+            n = contexts or int(os.environ.get("KDL_RESIZE_CTX", "4"))
+            self._free: queue.SimpleQueue = queue.SimpleQueue()
+            for _ in range(max(1, n)):
+                self._free.put(_Ctx(self._dev))
 
     def _tables(self, H: int, W: int):
         key = (H, W)
-        t = self._tabs.get(key)
-        if t is None:
-            ys, xs = nearest_indices(H, self.S), nearest_indices(W, self.S)
-            if self.device is not None:
-                ys = torch.from_numpy(ys).to(self._dev)
-                xs = torch.from_numpy(xs).to(self._dev)
-            t = self._tabs[key] = (ys, xs)
-            if len(self._tabs) > 256:
-                self._tabs.popitem(last=False)
-        else:
-            self._tabs.move_to_end(key)
-        return t
-
-    def _grow(self, n_in: int, n_out: int) -> None:
-        if n_in > self._cap_in:
-            self._cap_in = max(n_in, 2 * self._cap_in)
-            self._h_in = torch.empty(self._cap_in, dtype=torch.uint8).pin_memory()
-            self._d_in = torch.empty(self._cap_in, dtype=torch.uint8, device=self._dev)
-        if n_out > self._cap_out:
-            self._cap_out = max(n_out, 2 * self._cap_out)
-            self._h_out = torch.empty(self._cap_out, dtype=torch.uint8).pin_memory()
-            self._d_out = torch.empty(self._cap_out, dtype=torch.uint8, device=self._dev)
+        with self._tab_lock:
+            t = self._tabs.get(key)
+            if t is None:
+                ys, xs = nearest_indices(H, self.S), nearest_indices(W, self.S)
+                if self.device is not None:
+                    ys = torch.from_numpy(ys).to(self._dev)
+                    xs = torch.from_numpy(xs).to(self._dev)
+                t = self._tabs[key] = (ys, xs)
+                if len(self._tabs) > 256:
+                    self._tabs.popitem(last=False)
+            else:
+                self._tabs.move_to_end(key)
+            return t
 
     def __call__(self, x: np.ndarray) -> np.ndarray:
         assert x.dtype == np.uint8 and x.ndim == 4 and x.shape[3] == 3, (x.dtype, x.shape)
@@ -74,18 +89,21 @@ class Resizer:
             ys, xs = self._tables(H, W)
             return np.ascontiguousarray(x[:, ys][:, :, xs])
         n_in, n_out = x.size, n * S * S * 3
-        with self._lock:
-            self._grow(n_in, n_out)
-            ys, xs = self._tables(H, W)
-            self._h_in[:n_in].numpy()[:] = x.reshape(-1)
-            with torch.cuda.stream(self.stream):
-                self._d_in[:n_in].copy_(self._h_in[:n_in], non_blocking=True)
+        ys, xs = self._tables(H, W)
+        c = self._free.get()
+        try:
+            c.grow(n_in, n_out)
+            c.h_in[:n_in].numpy()[:] = x.reshape(-1)
+            with torch.cuda.device(self._dev), torch.cuda.stream(c.stream):
+                c.d_in[:n_in].copy_(c.h_in[:n_in], non_blocking=True)
                 _lib.lib().resize_nearest_u8(
-                    dict(src=_lib.ptr(self._d_in), dst=_lib.ptr(self._d_out), ytab=_lib.ptr(ys), xtab=_lib.ptr(xs),
-                         SH=H, SW=W, OH=S, OW=S, n=n), int(self.stream.cuda_stream))
-                self._h_out[:n_out].copy_(self._d_out[:n_out], non_blocking=True)
-            self.stream.synchronize()
-            return self._h_out[:n_out].numpy().reshape(n, S, S, 3).copy()
+                    dict(src=_lib.ptr(c.d_in), dst=_lib.ptr(c.d_out), ytab=_lib.ptr(ys), xtab=_lib.ptr(xs),
+                         SH=H, SW=W, OH=S, OW=S, n=n), int(c.stream.cuda_stream))
+                c.h_out[:n_out].copy_(c.d_out[:n_out], non_blocking=True)
+            c.stream.synchronize()
+            return c.h_out[:n_out].numpy().reshape(n, S, S, 3).copy()
+        finally:
+            self._free.put(c)
 
 
 class ImageRunner:

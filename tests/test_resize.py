@@ -34,3 +34,26 @@ def test_gpu_resize_kernel_equals_pil():
     for n, H, W in SHAPES + [(1, 534, 400)]:     # repeated size: cached tables, reused buffers
         x = np.random.default_rng(H * 3 + W).integers(0, 256, (n, H, W, 3), dtype=np.uint8)
         assert np.array_equal(r(x), _pil(x)), (n, H, W)
+
+
+@pytest.mark.gpu
+def test_gpu_resize_concurrent_requests_stay_exact():
+    """No global lock: 8 threads x 6 requests of mixed sizes on 3 contexts (each its own stream
+    and pinned staging) all equal PIL."""
+    import threading
+    r = Resizer(299, torch.cuda.current_device(), contexts=3)
+    errs = []
+
+    def worker(i):
+        rng = np.random.default_rng(100 + i)
+        for k in range(6):
+            H, W = [(534, 400), (299, 299), (1200, 300), (64, 77)][(i + k) % 4]
+            x = rng.integers(0, 256, (1 + k % 2, H, W, 3), dtype=np.uint8)
+            if not np.array_equal(r(x), _pil(x)):
+                errs.append((i, k, H, W))
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
