@@ -162,6 +162,7 @@ EntryBlockArgs eb_args(const py::dict& d) {
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
   a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.grid = I(d, "grid");
   a.steps = P<const int4>(d, "steps"); a.step_off = P<const int>(d, "step_off");
+  a.stamps = P<unsigned long long>(d, "stamps");
   if (!a.x || !a.y || !a.w1 || !a.b1 || !a.dw1 || !a.w2 || !a.b2 || !a.dw2 || !a.wr || !a.br)
     throw std::invalid_argument("entry_block: null pointer");
   return a;

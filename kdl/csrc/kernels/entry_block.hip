@@ -113,7 +113,7 @@ __device__ __forceinline__ s16x8 eb_frag(const uint16_t* wp, int nf, int kt, int
   return *(const s16x8*)(wp + ((long)(nf * kt + t) * 64 + lane) * 8);
 }
 
-template <int C0, int C1, int PC, int NFW, int PT, bool RELU1>
+template <int C0, int C1, int PC, int NFW, int PT, bool RELU1, bool STAMP = false>
 __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(EntryBlockArgs a) {
   using G = EbGeom<C0, C1, PC, NFW>;
   constexpr int NW = G::NW, KT0 = G::KT0, KT1 = G::KT1;
@@ -191,19 +191,38 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
   };
 
   u32x2 carry[NFW][Y2FR];                            // y2 row R+2 of the previous step (= this step's R), bf16
-  f32x4 accr[NFW];                                   // residual of the pooled row it was computed for
+  f32x4 accr[NFW];                                   // residual GEMM of the pooled row it was computed for
+  s16x8 wr[NFW][KT0];                                // residual 1x1/2 weights (register-resident)
+#pragma unroll
+  for (int n = 0; n < NFW; ++n)
+#pragma unroll
+    for (int t = 0; t < KT0; ++t) wr[n][t] = eb_frag(a.wr, NFW * w + n, KT0, t, lane);
   bool st_pend = false;                              // deferred output store of the previous step
   uint16_t* st_ptr = nullptr;
   u32x2 st_val[NFW];
 
+  // STAMP builds (diagnostics, tools/ebbench.py --stamps): thread 0 of workgroups < 8 records
+  // s_memtime after each barrier of its first 64 steps: [wg][step][B0, B1, B2, B3, end]
+  auto stamp = [&](int q, int ph) {
+    if constexpr (STAMP) {
+      if (tid == 0 && blockIdx.x < 8 && q - s0 < 64 && a.stamps)
+        a.stamps[((long)blockIdx.x * 64 + (q - s0)) * 5 + ph] = __builtin_amdgcn_s_memtime();
+    }
+  };
   dma_for(s0);
   for (int q = s0; q < s1; ++q) {
     int b, s, k, mode;
     decode(q, b, s, k, mode);
     const int R = 2 * k - PT;
     const int pc0 = s * PC;
+    // the residual this step's output adds: PT 1 computes it below (x row 2k is in the ring);
+    // PT 0 computed it in the previous step (x row 2k has left the ring by now)
+    f32x4 acco[NFW];
+#pragma unroll
+    for (int n = 0; n < NFW; ++n) acco[n] = accr[n];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();                                 // B0: x rows landed; previous step done
+    stamp(q, 0);
 
     // ---- P1: depthwise 1 -> A (y1 rows R+2, R+3); residual operands: pooled row k (PT 1: x row
     // 2k = R+1) or k+1 (PT 0: x row 2k+2 = R+2; x row 2k is no longer in the ring)
@@ -228,17 +247,18 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
     }
     if (PT == 1 ? mode == 2 : mode >= 1) {           // residual 1x1/2 conv of its pooled row
       const int xrow = R + 2 - PT, xcol = 2 * p16 + PT + 2;
-#pragma unroll 1
+#pragma unroll
       for (int n = 0; n < NFW; ++n) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < KT0; ++t)
-          acc = mfma16(eb_frag(a.wr, NFW * w + n, KT0, t, lane),
-                       *(const s16x8*)(xr + (xrow & 3) * XROW + (4 * t + q16) * PLB + xcol * 16), acc);
+          acc = mfma16(wr[n][t], *(const s16x8*)(xr + (xrow & 3) * XROW + (4 * t + q16) * PLB + xcol * 16), acc);
         accr[n] = acc;
+        if (PT == 1) acco[n] = acc;
       }
     }
     __syncthreads();                                 // B1: A (y1) complete; x ring free for the next DMA
+    stamp(q, 1);
 
     if (st_pend) {
 #pragma unroll
@@ -271,6 +291,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
       }
     }
     __syncthreads();                                 // B2: y1 rows R+2, R+3 written; A free
+    stamp(q, 2);
 
     if (mode == 0) continue;                         // warm-up 1: y1 only
     // ---- P3: depthwise 2 -> A (y2 rows R+1, R+2: fragments [row][col / 16])
@@ -292,6 +313,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
       }
     }
     __syncthreads();                                 // B3: A (y2) complete
+    stamp(q, 3);
 
     // ---- P4: GEMM2 + bias -> bf16 values; vertical max with the carried row
     const bool r0ok = (unsigned)R < (unsigned)H && mode == 2, r1ok = (unsigned)(R + 1) < (unsigned)H;
@@ -331,6 +353,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
           *(u32x2*)(pool + col * PCH + 16 * n + 4 * q16) = (u32x2){pack_bf16(vm[0], vm[1]), pack_bf16(vm[2], vm[3])};
       }
     }
+    stamp(q, 4);
     if (mode == 1) continue;                         // warm-up 2: carry (+ PT 0: residual) only
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own pool rows only: no barrier
     // horizontal 3/2 max: pooled column j reads y2 local cols 2j .. 2j+2
@@ -349,7 +372,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
           const uint32_t d0 = c0[e >> 1], d1 = c1[e >> 1], d2 = c2[e >> 1];
           const float m = (e & 1) ? fmaxf(fmaxf(bf_hi(d0), bf_hi(d1)), bf_hi(d2))
                                   : fmaxf(fmaxf(bf_lo(d0), bf_lo(d1)), bf_lo(d2));
-          o[e] = m + bf2f(f2bf(accr[n][e] + br4[e]));
+          o[e] = m + bf2f(f2bf(acco[n][e] + br4[e]));
         }
         st_val[n] = (u32x2){pack_bf16(o[0], o[1]), pack_bf16(o[2], o[3])};
       }
@@ -363,10 +386,13 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
 }
 
 // (C0, C1, PC, NFW, PT, RELU1) per id: 0 = block2 (147x147x64 -> 74x74x128), 1 = block3
-// (74x74x128 -> 37x37x256, the asymmetric 74 -> 37 pool: leading pad 0)
+// (74x74x128 -> 37x37x256, the asymmetric 74 -> 37 pool: leading pad 0); 100 + id: the same
+// with per-phase s_memtime stamps (EntryBlockArgs.stamps; diagnostics only)
 #define KDL_EB_CONFIGS(X)             \
   X(0, 64, 128, 15, 1, 1, false)      \
-  X(1, 128, 256, 13, 2, 0, true)
+  X(1, 128, 256, 13, 2, 0, true)      \
+  X(100, 64, 128, 15, 1, 1, false)    \
+  X(101, 128, 256, 13, 2, 0, true)
 
 int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds) {
   switch (cfg) {
@@ -396,7 +422,7 @@ hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
   switch (cfg) {
 #define KDL_EBCASE(id, c0_, c1_, pc_, nfw, pt, r_)                                                          \
   case id:                                                                                                 \
-    hipLaunchKernelGGL((entry_block_kernel<c0_, c1_, pc_, nfw, pt, r_>), dim3(a.grid),                      \
+    hipLaunchKernelGGL((entry_block_kernel<c0_, c1_, pc_, nfw, pt, r_, (id >= 100)>), dim3(a.grid),         \
                        dim3(64 * EbGeom<c0_, c1_, pc_, nfw>::NW), lds, s, a);                               \
     break;
     KDL_EB_CONFIGS(KDL_EBCASE)

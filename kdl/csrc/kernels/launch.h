@@ -83,6 +83,7 @@ struct EntryBlockArgs {
   int grid;               // workgroups (= len(step_off) - 1)
   const int4* steps;
   const int* step_off;
+  unsigned long long* stamps;   // stamping configs (id >= 100) only: [8 wg][64 steps][5 phases]
 };
 hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s);
 int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds);

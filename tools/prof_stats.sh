@@ -4,4 +4,4 @@
 out=$1; shift
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-exec rocprofv3 --kernel-trace --stats -d "$out" -o run -- "$@"
+exec rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- "$@"
