@@ -158,6 +158,7 @@ EntryBlockArgs eb_args(const py::dict& d) {
   a.x = P<const uint16_t>(d, "x"); a.y = P<uint16_t>(d, "y");
   a.w1 = P<const uint16_t>(d, "w1"); a.b1 = P<const float>(d, "b1"); a.dw1 = P<const float>(d, "dw1");
   a.w2 = P<const uint16_t>(d, "w2"); a.b2 = P<const float>(d, "b2"); a.dw2 = P<const float>(d, "dw2");
+  a.dwk1 = P<const uint16_t>(d, "dwk1"); a.dwk2 = P<const uint16_t>(d, "dwk2");
   a.wr = P<const uint16_t>(d, "wr"); a.br = P<const float>(d, "br");
   a.B = I(d, "B"); a.H = I(d, "H"); a.W = I(d, "W"); a.OH = I(d, "OH"); a.OW = I(d, "OW");
   a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.grid = I(d, "grid");

@@ -55,7 +55,8 @@ struct EbGeom {
   static constexpr int XDMA = XROW / 1024;          // 1 KiB DMA instructions per x row
   static constexpr int ABYTES = (KT0 * Y1F > KT1 * Y2F ? KT0 * Y1F : KT1 * Y2F) * 1024;
   static constexpr int PCOLS = 16 * Y2FR;           // pool row columns
-  static constexpr int DWQ = 4 * 40 * 4;            // LDS depthwise entries per k-step (4 lane groups x 40 words)
+  static constexpr int DWQ = 4 * 40 * 4;            // LDS depthwise entries per k-step (4 lane groups x 40 words;
+                                                    // the MFMA variant's pack_dw_entries take 1 KiB of it)
   // LDS map: the two depthwise A buffers alias (A1 is read before the barrier that precedes
   // A2's writes, A2 before the next step's first barrier)
   static constexpr int OFF_X = 0;
@@ -109,11 +110,42 @@ __device__ __forceinline__ s16x8 eb_dw8(Tap tap, const uint32_t* wq) {
   return __builtin_bit_cast(s16x8, o);
 }
 
+// depthwise 3x3 of a 16-pixel x 32-channel unit on the MATRIX cores (the block-diagonal operand of
+// sepconv_ws.hip): per 16-channel group g, 5 MFMAs over tap pairs. Lane (p16, kb) feeds tap
+// 2j + (kb >> 1) of chunk 2g + (kb & 1); tap(g, ti) -> that 16-B input; ent(g) -> the 16-B entry
+// (pack_dw_entries) of channel 16g + p16, tap parity kb >> 1. The C fragment [16 ch][16 px] is
+// written transposed into the unit's lane-linear A fragment at dst.
+template <bool RELU, class Tap, class Ent>
+__device__ __forceinline__ void eb_dw_mfma(Tap tap, Ent ent, uint8_t* dst, int lane, const uint32_t (&sel)[2][4]) {
+  const int p16 = lane & 15, kb = lane >> 4, par = kb >> 1;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const u32x4 we = ent(g);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int ti = 2 * j + par;
+      u32x4 v = ti < 9 ? tap(g, ti) : (u32x4){0u, 0u, 0u, 0u};
+      if constexpr (RELU) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
+      }
+      const uint32_t wd = we[j >> 1];
+      u32x4 wf;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) wf[d] = __builtin_amdgcn_perm(wd, wd, sel[j & 1][d]);
+      acc = mfma16(__builtin_bit_cast(s16x8, wf), __builtin_bit_cast(s16x8, v), acc);
+    }
+    *(u32x2*)(dst + (p16 + 16 * (2 * g + par)) * 16 + 8 * (kb & 1)) =
+        (u32x2){pack_bf16(acc[0], acc[1]), pack_bf16(acc[2], acc[3])};
+  }
+}
+
 __device__ __forceinline__ s16x8 eb_frag(const uint16_t* wp, int nf, int kt, int t, int lane) {
   return *(const s16x8*)(wp + ((long)(nf * kt + t) * 64 + lane) * 8);
 }
 
-template <int C0, int C1, int PC, int NFW, int PT, bool RELU1, bool STAMP = false>
+template <int C0, int C1, int PC, int NFW, int PT, bool RELU1, bool STAMP = false, bool DWM = false>
 __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(EntryBlockArgs a) {
   using G = EbGeom<C0, C1, PC, NFW>;
   constexpr int NW = G::NW, KT0 = G::KT0, KT1 = G::KT1;
@@ -141,7 +173,16 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
   uint32_t* const dwl = (uint32_t*)(smem + G::OFF_DW);
   float* const bl = (float*)(smem + G::OFF_B);
 
-  // ---- depthwise weight entries -> LDS: [k-step][lane group q][tap pair j][channel e] bf16x2
+  // ---- depthwise weight entries -> LDS. VALU variant: [k-step][lane group q][tap pair j][channel e]
+  // bf16x2; MFMA variant (DWM): pack_dw_entries' [k-step][g][n][parity][8] bf16, 1 KiB per k-step
+  if constexpr (DWM) {
+    for (int i = tid; i < (KT0 + KT1) * 64; i += 64 * NW) {
+      const int t = i / 64;
+      const u32x4 v = t < KT0 ? *(const u32x4*)((const uint8_t*)a.dwk1 + t * 1024 + (i % 64) * 16)
+                              : *(const u32x4*)((const uint8_t*)a.dwk2 + (t - KT0) * 1024 + (i % 64) * 16);
+      *(u32x4*)((uint8_t*)dwl + t * G::DWQ + (i % 64) * 16) = v;
+    }
+  } else
   for (int i = tid; i < (KT0 + KT1) * 4 * 40; i += 64 * NW) {
     const int t = i / 160, q = (i / 40) % 4, j = (i % 40) / 8, e = i % 8;
     const bool second = t >= KT0;
@@ -164,6 +205,19 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
   // this lane's 4 accumulator channels of output slice n: bias (LDS) of GEMM g (0 pw1, 1 pw2, 2 residual)
   auto bias = [&](int g, int n) { return *(const float4*)(bl + g * C1 + PCH * w + 16 * n + 4 * q16); };
   const int t1 = w % KT0, t2 = w % KT1;              // every depthwise unit of this wave uses these k-steps
+  uint32_t sel[2][4];                                // DWM: v_perm selectors of the block-diagonal operand
+  {
+    const bool wv = (p16 >> 3) == (q16 & 1);
+    const int e = p16 & 7;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t pair = (2u * jp) | ((2u * jp + 1u) << 8);
+        const uint32_t val = (e & 1) ? (0x0c0cu | (pair << 16)) : (0x0c0c0000u | pair);
+        sel[jp][d] = (wv && (e >> 1) == d) ? val : 0x0c0c0c0cu;
+      }
+  }
   // ---- x row DMA: row r of image b, strip columns from global col gx0, into ring slot r & 3
   auto dma_rows = [&](int b, int gx0, int r0, int nr) {
     for (int ii = w; ii < nr * G::XDMA; ii += NW) {
@@ -237,11 +291,22 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
           pi = pi < 2 * Y1C ? pi : 2 * Y1C - 1;
           const int rr = pi >= Y1C, col = pi - rr * Y1C;
           const int row = R + 2 + rr;
-          const uint8_t* base = xr + (4 * t1 + q16) * PLB + col * 16;
-          auto tap = [&](int ti) {
-            return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * XROW + (ti % 3) * 16);
-          };
-          *(s16x8*)(Ab + (t1 * Y1F + f) * 1024 + lane * 16) = eb_dw8<RELU1>(tap, wq);
+          if constexpr (DWM) {
+            const uint8_t* base = xr + (4 * t1 + (q16 & 1)) * PLB + col * 16;
+            auto tap = [&](int g, int ti) {
+              return *(const u32x4*)(base + 2 * g * PLB + ((row - 1 + ti / 3) & 3) * XROW + (ti % 3) * 16);
+            };
+            auto ent = [&](int g) {
+              return *(const u32x4*)((const uint8_t*)dwl + t1 * G::DWQ + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
+            };
+            eb_dw_mfma<RELU1>(tap, ent, Ab + (t1 * Y1F + f) * 1024, lane, sel);
+          } else {
+            const uint8_t* base = xr + (4 * t1 + q16) * PLB + col * 16;
+            auto tap = [&](int ti) {
+              return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * XROW + (ti % 3) * 16);
+            };
+            *(s16x8*)(Ab + (t1 * Y1F + f) * 1024 + lane * 16) = eb_dw8<RELU1>(tap, wq);
+          }
         }
       }
     }
@@ -304,11 +369,22 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
           const int f = u / KT1;
           const int rr = f / Y2FR, col = (f % Y2FR) * 16 + p16;
           const int row = R + 1 + rr;
-          const uint8_t* base = y1r + (4 * t2 + q16) * PLB + col * 16;
-          auto tap = [&](int ti) {
-            return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * Y1ROW + (ti % 3) * 16);
-          };
-          *(s16x8*)(Ab + (t2 * Y2F + f) * 1024 + lane * 16) = eb_dw8<false>(tap, wq);
+          if constexpr (DWM) {
+            const uint8_t* base = y1r + (4 * t2 + (q16 & 1)) * PLB + col * 16;
+            auto tap = [&](int g, int ti) {
+              return *(const u32x4*)(base + 2 * g * PLB + ((row - 1 + ti / 3) & 3) * Y1ROW + (ti % 3) * 16);
+            };
+            auto ent = [&](int g) {
+              return *(const u32x4*)((const uint8_t*)dwl + (KT0 + t2) * G::DWQ + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
+            };
+            eb_dw_mfma<false>(tap, ent, Ab + (t2 * Y2F + f) * 1024, lane, sel);
+          } else {
+            const uint8_t* base = y1r + (4 * t2 + q16) * PLB + col * 16;
+            auto tap = [&](int ti) {
+              return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * Y1ROW + (ti % 3) * 16);
+            };
+            *(s16x8*)(Ab + (t2 * Y2F + f) * 1024 + lane * 16) = eb_dw8<false>(tap, wq);
+          }
         }
       }
     }
@@ -387,12 +463,17 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
 
 // (C0, C1, PC, NFW, PT, RELU1) per id: 0 = block2 (147x147x64 -> 74x74x128), 1 = block3
 // (74x74x128 -> 37x37x256, the asymmetric 74 -> 37 pool: leading pad 0); 100 + id: the same
-// with per-phase s_memtime stamps (EntryBlockArgs.stamps; diagnostics only)
+// with per-phase s_memtime stamps (EntryBlockArgs.stamps; diagnostics only); 2, 3: 0, 1 with the
+// depthwise convs on the matrix cores (block-diagonal operand) instead of the VALU
 #define KDL_EB_CONFIGS(X)             \
   X(0, 64, 128, 15, 1, 1, false)      \
   X(1, 128, 256, 13, 2, 0, true)      \
+  X(2, 64, 128, 15, 1, 1, false)      \
+  X(3, 128, 256, 13, 2, 0, true)      \
   X(100, 64, 128, 15, 1, 1, false)    \
-  X(101, 128, 256, 13, 2, 0, true)
+  X(101, 128, 256, 13, 2, 0, true)    \
+  X(102, 64, 128, 15, 1, 1, false)    \
+  X(103, 128, 256, 13, 2, 0, true)
 
 int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds) {
   switch (cfg) {
@@ -422,7 +503,7 @@ hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
   switch (cfg) {
 #define KDL_EBCASE(id, c0_, c1_, pc_, nfw, pt, r_)                                                          \
   case id:                                                                                                 \
-    hipLaunchKernelGGL((entry_block_kernel<c0_, c1_, pc_, nfw, pt, r_, (id >= 100)>), dim3(a.grid),         \
+    hipLaunchKernelGGL((entry_block_kernel<c0_, c1_, pc_, nfw, pt, r_, (id >= 100), (id % 100 >= 2)>), dim3(a.grid),         \
                        dim3(64 * EbGeom<c0_, c1_, pc_, nfw>::NW), lds, s, a);                               \
     break;
     KDL_EB_CONFIGS(KDL_EBCASE)

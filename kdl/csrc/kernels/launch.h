@@ -77,6 +77,8 @@ struct EntryBlockArgs {
   const uint16_t* w2;     // sepconv2 pointwise, packed [C1/16][C1/32][64][8]
   const float* b2;
   const float* dw2;       // [9][C1]
+  const uint16_t* dwk1;   // the same depthwise weights as pack_dw_entries (MFMA depthwise configs)
+  const uint16_t* dwk2;
   const uint16_t* wr;     // residual 1x1/2 conv, packed [C1/16][C0/32][64][8]
   const float* br;
   int B, H, W, OH, OW, ldx, ldy;

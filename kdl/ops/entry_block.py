@@ -73,7 +73,7 @@ class EntryBlock:
         assert res.cin_pad == c0 and res.n == c1 and not sep2.relu_in and sep1.relu_out == 1 and sep2.relu_out == 0
         self.name, self.cfg, self.c0, self.c1, self.pc, self.lds = name, cfg, c0, c1, pc, lds
         self.relu_in = bool(sep1.relu_in)
-        assert self.relu_in == (cfg == 1), "config 0 is block2 (no pre-activation), 1 is block3 (ReLU first)"
+        assert self.relu_in == (cfg % 2 == 1), "even configs: block2 (no pre-activation); odd: block3 (ReLU first)"
         self.sep1, self.sep2, self.res = sep1, sep2, res
         self.device = torch.device(device)
         self.grid = grid
@@ -93,6 +93,7 @@ class EntryBlock:
         st, of, grid = self.plan(B, OH, OW)
         return dict(x=x, y=y, w1=_lib.ptr(self.sep1.wp), b1=_lib.ptr(self.sep1.bias), dw1=_lib.ptr(self.sep1.dww),
                     w2=_lib.ptr(self.sep2.wp), b2=_lib.ptr(self.sep2.bias), dw2=_lib.ptr(self.sep2.dww),
+                    dwk1=_lib.ptr(self.sep1.dwk), dwk2=_lib.ptr(self.sep2.dwk),
                     wr=_lib.ptr(self.res.wp), br=_lib.ptr(self.res.bias), B=B, H=H, W=W, OH=OH, OW=OW,
                     ldx=self.c0, ldy=self.c1, grid=grid, steps=_lib.ptr(st), step_off=_lib.ptr(of))
 
