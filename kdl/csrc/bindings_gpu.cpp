@@ -341,9 +341,9 @@ PYBIND11_MODULE(_C, m) {
     chk(entry_block(cfg, a, S(s)), "entry_block");
   });
   m.def("entry_block_config", [](int cfg) {
-    int c0 = 0, c1 = 0, pc = 0, lds = 0;
-    if (entry_block_config(cfg, &c0, &c1, &pc, &lds) != 0) throw std::out_of_range("bad entry_block config");
-    return py::make_tuple(c0, c1, pc, lds);
+    int c0 = 0, c1 = 0, pc = 0, lds = 0, occ = 0;
+    if (entry_block_config(cfg, &c0, &c1, &pc, &lds, &occ) != 0) throw std::out_of_range("bad entry_block config");
+    return py::make_tuple(c0, c1, pc, lds, occ);
   });
   m.def("gemm_f8", [](int cfg, py::dict d, uintptr_t s) {
     const auto a = f8_args(d);

@@ -38,7 +38,9 @@ namespace kdl {
 
 __device__ __attribute__((aligned(16))) uint8_t eb_zeros[256];
 
-template <int C0, int C1, int PC, int NFW>
+constexpr int EB_MAX_STEPS = 160;                  // steps per workgroup (host plan checks it)
+
+template <int C0, int C1, int PC, int NFW, bool DWM = false>
 struct EbGeom {
   static constexpr int Y2C = 2 * PC + 1;            // y2 columns a strip needs
   static constexpr int Y1C = Y2C + 2;               // y1 columns
@@ -55,8 +57,8 @@ struct EbGeom {
   static constexpr int XDMA = XROW / 1024;          // 1 KiB DMA instructions per x row
   static constexpr int ABYTES = (KT0 * Y1F > KT1 * Y2F ? KT0 * Y1F : KT1 * Y2F) * 1024;
   static constexpr int PCOLS = 16 * Y2FR;           // pool row columns
-  static constexpr int DWQ = 4 * 40 * 4;            // LDS depthwise entries per k-step (4 lane groups x 40 words;
-                                                    // the MFMA variant's pack_dw_entries take 1 KiB of it)
+  static constexpr int DWQ = DWM ? 1024 : 640;      // LDS depthwise entries per k-step: 4 lane groups x 40 words
+                                                    // (VALU), or pack_dw_entries' 1 KiB (MFMA variant)
   // LDS map: the two depthwise A buffers alias (A1 is read before the barrier that precedes
   // A2's writes, A2 before the next step's first barrier)
   static constexpr int OFF_X = 0;
@@ -65,7 +67,8 @@ struct EbGeom {
   static constexpr int OFF_P = OFF_A + ABYTES;      // per-wave pool rows [NW][PCOLS][16*NFW] bf16
   static constexpr int OFF_DW = OFF_P + NW * PCOLS * 16 * NFW * 2;
   static constexpr int OFF_B = OFF_DW + (KT0 + KT1) * DWQ;   // biases [3][C1] fp32
-  static constexpr int BYTES = OFF_B + 3 * C1 * 4;
+  static constexpr int OFF_S = OFF_B + 3 * C1 * 4;  // this workgroup's step table (int4 x MAX_STEPS)
+  static constexpr int BYTES = OFF_S + 16 * EB_MAX_STEPS;
   static_assert(XROW % 1024 == 0, "whole DMA instructions per x row");
   static_assert(C0 % 32 == 0 && C1 % (16 * NFW) == 0 && NW <= 16, "channel tiling");
   static_assert(BYTES <= 160 * 1024, "LDS");
@@ -145,9 +148,9 @@ __device__ __forceinline__ s16x8 eb_frag(const uint16_t* wp, int nf, int kt, int
   return *(const s16x8*)(wp + ((long)(nf * kt + t) * 64 + lane) * 8);
 }
 
-template <int C0, int C1, int PC, int NFW, int PT, bool RELU1, bool STAMP = false, bool DWM = false>
-__global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(EntryBlockArgs a) {
-  using G = EbGeom<C0, C1, PC, NFW>;
+template <int C0, int C1, int PC, int NFW, int PT, bool RELU1, bool STAMP = false, bool DWM = false, int OCC = 1>
+__global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void entry_block_kernel(EntryBlockArgs a) {
+  using G = EbGeom<C0, C1, PC, NFW, DWM>;
   constexpr int NW = G::NW, KT0 = G::KT0, KT1 = G::KT1;
   constexpr int PLB = G::PLB, XROW = G::XROW, Y1ROW = G::Y1ROW;
   constexpr int Y1C = G::Y1C, Y2C = G::Y2C, XC = G::XC, PLP = G::PLP;
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
   const int q16 = lane >> 4, p16 = lane & 15;
   const int H = a.H, W = a.W;
   const int s0 = a.step_off[blockIdx.x], s1 = a.step_off[blockIdx.x + 1];
-  if (s0 >= s1) return;                              // uniform: this workgroup has no work
+  if (s0 >= s1 || s1 - s0 > EB_MAX_STEPS) return;   // uniform: no work (or a plan the host must reject)
 
   uint8_t* const xr = smem + G::OFF_X;
   uint8_t* const y1r = smem + G::OFF_Y1;
@@ -172,6 +175,10 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
   uint16_t* const pool = (uint16_t*)(smem + G::OFF_P) + w * (PCOLS * PCH);
   uint32_t* const dwl = (uint32_t*)(smem + G::OFF_DW);
   float* const bl = (float*)(smem + G::OFF_B);
+  int4* const stl = (int4*)(smem + G::OFF_S);
+  // the step table goes to LDS once: decoding a step from global memory put an L2 round trip
+  // on every step's critical path twice (measured ~3k cycles per step, tools/ebbench.py --stamps)
+  for (int i = tid; i < s1 - s0; i += 64 * NW) stl[i] = a.steps[s0 + i];
 
   // ---- depthwise weight entries -> LDS. VALU variant: [k-step][lane group q][tap pair j][channel e]
   // bf16x2; MFMA variant (DWM): pack_dw_entries' [k-step][g][n][parity][8] bf16, 1 KiB per k-step
@@ -230,7 +237,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
     }
   };
   auto decode = [&](int q, int& b, int& s, int& k, int& mode) {
-    const int4 e = a.steps[q];
+    const int4 e = stl[q - s0];
     b = e.x; s = e.y; k = e.z; mode = e.w;
   };
   // pooled row k pools y2 rows R..R+2, R = 2k - PT; a step computes y1 rows R+2, R+3 from x rows
@@ -263,6 +270,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
         a.stamps[((long)blockIdx.x * 64 + (q - s0)) * 5 + ph] = __builtin_amdgcn_s_memtime();
     }
   };
+  __syncthreads();                                   // step table, weights, biases in LDS
   dma_for(s0);
   for (int q = s0; q < s1; ++q) {
     int b, s, k, mode;
@@ -461,24 +469,28 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW))) void entry_block_kernel(Ent
   }
 }
 
-// (C0, C1, PC, NFW, PT, RELU1) per id: 0 = block2 (147x147x64 -> 74x74x128), 1 = block3
+// (C0, C1, PC, NFW, PT, RELU1, DWM, OCC = workgroups per CU) per id: 0 = block2 (147x147x64 -> 74x74x128), 1 = block3
 // (74x74x128 -> 37x37x256, the asymmetric 74 -> 37 pool: leading pad 0); 100 + id: the same
 // with per-phase s_memtime stamps (EntryBlockArgs.stamps; diagnostics only); 2, 3: 0, 1 with the
-// depthwise convs on the matrix cores (block-diagonal operand) instead of the VALU
-#define KDL_EB_CONFIGS(X)             \
-  X(0, 64, 128, 15, 1, 1, false)      \
-  X(1, 128, 256, 13, 2, 0, true)      \
-  X(2, 64, 128, 15, 1, 1, false)      \
-  X(3, 128, 256, 13, 2, 0, true)      \
-  X(100, 64, 128, 15, 1, 1, false)    \
-  X(101, 128, 256, 13, 2, 0, true)    \
-  X(102, 64, 128, 15, 1, 1, false)    \
-  X(103, 128, 256, 13, 2, 0, true)
+// depthwise convs on the matrix cores (block-diagonal operand) instead of the VALU (block2 only:
+// block3's LDS map has no room for the larger entries); 4, 5: block2
+// with 13-column strips, small enough (LDS, <= 128 VGPRs) for two workgroups per CU
+#define KDL_EB_CONFIGS(X)                          \
+  X(0, 64, 128, 15, 1, 1, false, false, 1)         \
+  X(1, 128, 256, 13, 2, 0, true, false, 1)         \
+  X(2, 64, 128, 15, 1, 1, false, true, 1)          \
+  X(4, 64, 128, 13, 1, 1, false, false, 2)         \
+  X(5, 64, 128, 13, 1, 1, false, true, 2)          \
+  X(100, 64, 128, 15, 1, 1, false, false, 1)       \
+  X(101, 128, 256, 13, 2, 0, true, false, 1)       \
+  X(102, 64, 128, 15, 1, 1, false, true, 1)        \
+  X(104, 64, 128, 13, 1, 1, false, false, 2)       \
+  X(105, 64, 128, 13, 1, 1, false, true, 2)
 
-int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds) {
+int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds, int* occ) {
   switch (cfg) {
-#define KDL_EBINFO(id, c0_, c1_, pc_, nfw, pt, r_) \
-  case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbGeom<c0_, c1_, pc_, nfw>::BYTES; return 0;
+#define KDL_EBINFO(id, c0_, c1_, pc_, nfw, pt, r_, dwm, occ_) \
+  case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbGeom<c0_, c1_, pc_, nfw, dwm>::BYTES; *occ = occ_; return 0;
     KDL_EB_CONFIGS(KDL_EBINFO)
 #undef KDL_EBINFO
     default: return -1;
@@ -487,7 +499,7 @@ int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds) {
 
 static int eb_pad(int cfg) {
   switch (cfg) {
-#define KDL_EBPAD(id, c0_, c1_, pc_, nfw, pt, r_) case id: return pt;
+#define KDL_EBPAD(id, c0_, c1_, pc_, nfw, pt, r_, dwm, occ_) case id: return pt;
     KDL_EB_CONFIGS(KDL_EBPAD)
 #undef KDL_EBPAD
     default: return -1;
@@ -495,16 +507,16 @@ static int eb_pad(int cfg) {
 }
 
 hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
-  int c0, c1, pc, lds;
-  if (entry_block_config(cfg, &c0, &c1, &pc, &lds) != 0 || a.ldx != c0 || a.ldy != c1 || a.grid < 1 ||
+  int c0, c1, pc, lds, occ;
+  if (entry_block_config(cfg, &c0, &c1, &pc, &lds, &occ) != 0 || a.ldx != c0 || a.ldy != c1 || a.grid < 1 ||
       a.OH != (a.H - 1) / 2 + 1 || a.OW != (a.W - 1) / 2 + 1 || a.H != a.W || !a.steps || !a.step_off)
     return hipErrorInvalidValue;
   if (eb_pad(cfg) != (a.H % 2)) return hipErrorInvalidValue;   // TF 'same': leading pad 1 iff odd size
   switch (cfg) {
-#define KDL_EBCASE(id, c0_, c1_, pc_, nfw, pt, r_)                                                          \
+#define KDL_EBCASE(id, c0_, c1_, pc_, nfw, pt, r_, dwm, occ_)                                               \
   case id:                                                                                                 \
-    hipLaunchKernelGGL((entry_block_kernel<c0_, c1_, pc_, nfw, pt, r_, (id >= 100), (id % 100 >= 2)>), dim3(a.grid),         \
-                       dim3(64 * EbGeom<c0_, c1_, pc_, nfw>::NW), lds, s, a);                               \
+    hipLaunchKernelGGL((entry_block_kernel<c0_, c1_, pc_, nfw, pt, r_, (id >= 100), dwm, occ_>), dim3(a.grid), \
+                       dim3(64 * EbGeom<c0_, c1_, pc_, nfw, dwm>::NW), lds, s, a);                               \
     break;
     KDL_EB_CONFIGS(KDL_EBCASE)
 #undef KDL_EBCASE

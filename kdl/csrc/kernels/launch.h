@@ -88,7 +88,7 @@ struct EntryBlockArgs {
   unsigned long long* stamps;   // stamping configs (id >= 100) only: [8 wg][64 steps][5 phases]
 };
 hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s);
-int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds);
+int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds, int* occ);
 
 // cfg >= C3_CFG_BASE: 3x3 'valid' conv over 2-D tiles with an LDS halo patch (MODE_CONV, cin 32 only,
 // conv3x3_2d.hip: Xception block1_conv2).

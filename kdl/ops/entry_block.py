@@ -21,10 +21,11 @@ from .conv import MODE_DW, MODE_PW, ConvGemmLayer
 
 # mode of a step (EntryBlockArgs.steps[i].w)
 WARM_Y1, WARM_Y2, OUT = 0, 1, 2
+MAX_STEPS = 160          # entry_block.hip EB_MAX_STEPS: a workgroup's step table lives in LDS
 
 
-def entry_block_config(cfg: int) -> tuple[int, int, int, int]:
-    """(C0, C1, PC, LDS bytes) of a kernel config (mirror of KDL_EB_CONFIGS)."""
+def entry_block_config(cfg: int) -> tuple[int, int, int, int, int]:
+    """(C0, C1, PC, LDS bytes, workgroups per CU) of a kernel config (mirror of KDL_EB_CONFIGS)."""
     return tuple(_lib.lib().entry_block_config(cfg))
 
 
@@ -67,13 +68,13 @@ class EntryBlock:
                  device="cuda", grid: int | None = None):
         """``grid``: workgroups (default: one per CU); ``cfg``: kernel config (default: by channels)."""
         cfg = CONFIGS[(sep1.cin_pad, sep1.n)] if cfg is None else cfg
-        c0, c1, pc, lds = entry_block_config(cfg)
+        c0, c1, pc, lds, occ = entry_block_config(cfg)
         assert sep1.mode == MODE_DW and sep2.mode == MODE_DW and res.mode == MODE_PW and res.stride == 2, name
         assert sep1.cin_pad == c0 and sep1.n == c1 and sep2.cin_pad == c1 and sep2.n == c1, (name, c0, c1)
         assert res.cin_pad == c0 and res.n == c1 and not sep2.relu_in and sep1.relu_out == 1 and sep2.relu_out == 0
-        self.name, self.cfg, self.c0, self.c1, self.pc, self.lds = name, cfg, c0, c1, pc, lds
+        self.name, self.cfg, self.c0, self.c1, self.pc, self.lds, self.occ = name, cfg, c0, c1, pc, lds, occ
         self.relu_in = bool(sep1.relu_in)
-        assert self.relu_in == (cfg % 2 == 1), "even configs: block2 (no pre-activation); odd: block3 (ReLU first)"
+        assert self.relu_in == (c0 == 128), "block2 (64 -> 128): no pre-activation; block3 (128 -> 256): ReLU first"
         self.sep1, self.sep2, self.res = sep1, sep2, res
         self.device = torch.device(device)
         self.grid = grid
@@ -82,7 +83,8 @@ class EntryBlock:
     def plan(self, B: int, OH: int, OW: int) -> tuple[torch.Tensor, torch.Tensor, int]:
         key = (B, OH, OW)
         if key not in self._plans:
-            steps, off = plan_steps(B, OH, OW, self.pc, self.grid or _lib.num_cus(self.device))
+            steps, off = plan_steps(B, OH, OW, self.pc, self.grid or self.occ * _lib.num_cus(self.device))
+            assert max(b - a for a, b in zip(off, off[1:])) <= MAX_STEPS, "workgroup step table > EB_MAX_STEPS"
             st = torch.tensor(steps, dtype=torch.int32).reshape(-1, 4).to(self.device)
             of = torch.tensor(off, dtype=torch.int32).to(self.device)
             self._plans[key] = (st, of, len(off) - 1)

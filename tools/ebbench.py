@@ -23,8 +23,8 @@ def stamps(p, blocks, B):
         b = X.SPEC[blk - 1]
         s1, s2, r = XE._sep(p, b.main[0], "cuda"), XE._sep(p, b.main[1], "cuda"), XE._pw(p, b.res_conv, "cuda")
         H, C0 = geom[blk]
-        base = CONFIGS[(C0, s1.n)]
-        for cfg in (base, 100 + base, base + 2, 102 + base):
+        cfgs = [0, 2, 4, 5] if blk == 2 else [1]
+        for cfg in [c for b in cfgs for c in (b, 100 + b)]:
             eb = EntryBlock(f"block{blk}", s1, s2, r, cfg=cfg)
             x = torch.randn(B, H, H, C0, device="cuda").to(torch.bfloat16)
             y = torch.empty(B, (H - 1) // 2 + 1, (H - 1) // 2 + 1, s1.n, dtype=torch.bfloat16, device="cuda")

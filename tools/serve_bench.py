@@ -62,7 +62,8 @@ def _launch_procs(a):
         port = s.getsockname()[1]
     sizes = ",".join(str(b) for b in (1, 2, 4, 8, 16, 32, 64) if b <= a.max_batch)
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-    cmd = [sys.executable, "-m", "kdl.serving", f"--procs={a.procs}", f"--port={port}", "--rest_api_port=0",
+    topo = ([f"--scatter=rccl", f"--dp_world={a.dp_world}"] if a.scatter == "rccl" else [f"--procs={a.procs}"])
+    cmd = [sys.executable, "-m", "kdl.serving", *topo, f"--port={port}", "--rest_api_port=0",
            f"--model_base_path={base}", f"--device={a.device}", "--host=127.0.0.1", f"--allowed_batch_sizes={sizes}",
            f"--batch_timeout_micros={a.timeout_us}", f"--grpc_max_threads={max(64, a.clients * 2)}",
            f"--warm_signatures={a.signature}"]
@@ -72,7 +73,8 @@ def _launch_procs(a):
                          stderr=subprocess.DEVNULL, start_new_session=True)
     target = f"127.0.0.1:{port}"
     seen, t_end = set(), time.time() + 600
-    while len(seen) < a.procs and time.time() < t_end and p.poll() is None:
+    want = 1 if a.scatter == "rccl" else a.procs
+    while len(seen) < want and time.time() < t_end and p.poll() is None:
         ch = grpc.insecure_channel(target, options=[("grpc.use_local_subchannel_pool", 1)])
         try:
             resp, call = ch.unary_unary("/grpc.health.v1.Health/Check").with_call(b"", timeout=5)
@@ -82,8 +84,8 @@ def _launch_procs(a):
             time.sleep(0.5)
         finally:
             ch.close()
-    if len(seen) < a.procs:
-        raise SystemExit(f"only {len(seen)} of {a.procs} server processes came up")
+    if len(seen) < want:
+        raise SystemExit(f"only {len(seen)} of {want} server processes came up")
     return p, target
 
 
@@ -107,6 +109,12 @@ def main(argv=None) -> int:
                     help="serve from `python -m kdl.serving --procs N` (N processes sharing the port via "
                          "SO_REUSEPORT, one per GPU mod the visible GPUs) instead of an in-process server; "
                          "every client opens its own connection")
+    ap.add_argument("--scatter", choices=["host", "rccl"], default="host",
+                    help="rccl: serve from `python -m kdl.serving --scatter rccl --dp_world W` (one front-end, "
+                         "the native RCCL data-parallel executor, serving/dp.py)")
+    ap.add_argument("--dp-world", type=int, default=1)
+    ap.add_argument("--stages", action="store_true",
+                    help="in-process server: print the native executor's mean per-stage times")
     ap.add_argument("--client-procs", type=int, default=0,
                     help="run the clients in this many spawned processes (0: threads of the server "
                          "process, which then share its GIL with the server's handlers)")
@@ -134,7 +142,7 @@ def main(argv=None) -> int:
     srv = None
     launcher = None
     target = a.target
-    if target is None and a.procs:
+    if target is None and (a.procs or a.scatter == "rccl"):
         launcher, target = _launch_procs(a)
     if target is None:
         import tempfile
@@ -192,12 +200,22 @@ def main(argv=None) -> int:
            "p50_ms": round(statistics.median(lat) * 1e3, 2),
            "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2)}
     if srv is not None:
-        st = srv.manager.get("clothing-model").runner(a.signature).batcher.stats()
+        run = srv.manager.get("clothing-model").runner(a.signature)
+        st = run.batcher.stats()
         res["mean_batch"] = round(st["items"] / max(1, st["batches"]), 2)
+        if a.stages:
+            for ex in run.executors:
+                nat = getattr(ex, "native", None)
+                if nat is not None:
+                    sg = nat.stats()["stages"]
+                    res.setdefault("stage_mean_ms", {})[ex.name] = {
+                        k: round(v["sum_ms"] / max(1, v["count"]), 3) for k, v in sg.items()}
         srv.stop(0)
     if launcher is not None:
         import signal
         res["procs"] = a.procs
+        if a.scatter == "rccl":
+            res["topology"] = f"scatter rccl, dp_world {a.dp_world}"
         os.killpg(launcher.pid, signal.SIGTERM)
         launcher.wait(timeout=60)
     print(json.dumps(res), flush=True)
