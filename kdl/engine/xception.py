@@ -42,8 +42,13 @@ class XceptionEngine(EngineBase):
         self.in_kind = in_kind
         self.head = head
         # fused entry blocks (entry_block.hip): block numbers lowered to one launch each
+        # KDL_ENTRY_BLOCK: "1" = blocks 2 and 3, or a list "2,3" / "2:4,3" (block[:kernel config])
         eb = os.environ.get("KDL_ENTRY_BLOCK", "0")
-        self.fused_blocks = {2, 3} if eb == "1" else {int(v) for v in eb.split(",") if v.strip() and v != "0"}
+        spec = "2,3" if eb == "1" else ("" if eb == "0" else eb)
+        self.fused_blocks = {}
+        for v in filter(None, (x.strip() for x in spec.split(","))):
+            blk, _, cfg = v.partition(":")
+            self.fused_blocks[int(blk)] = int(cfg) if cfg else None
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
@@ -95,7 +100,7 @@ class XceptionEngine(EngineBase):
                 if bi + 1 in self.fused_blocks:
                     from ..ops.entry_block import EntryBlock
                     s1, s2 = (self._sep(p, op, dev) for op in blk.main)
-                    fb = EntryBlock(f"block{bi + 1}", s1, s2, lay, device=dev)
+                    fb = EntryBlock(f"block{bi + 1}", s1, s2, lay, cfg=self.fused_blocks[bi + 1], device=dev)
                     self.steps.append(Step("block", f"block{bi + 1}", src=cur, dst=out, geom=(H, H, oh, oh),
                                            extra=dict(eb=fb)))
                     self.shapes[out] = (oh, oh, s2.ldy)

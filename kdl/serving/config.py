@@ -74,6 +74,7 @@ class ServerConfig:
     procs: int = 1
     gpu_index: int = -1
     warm_signatures: list[str] = field(default_factory=list)   # built at load, besides serving_default
+    f32_exact_u8: bool = True    # f32 requests that are exactly x/127.5-1 of 8-bit pixels ride the uint8 path
     # --scatter rccl: ONE front-end (rank 0) + one process per GPU, batches scattered / logits
     # gathered over RCCL (serving/dp.py); host = every process ingests its own requests
     scatter: str = "host"
@@ -143,6 +144,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "SO_REUSEPORT, so the kernel spreads client connections over them; process i "
                          "serves GPU i (mod the visible GPUs)")
     ap.add_argument("--gpu_index", type=int, default=-1, help=argparse.SUPPRESS)   # set by the --procs launcher
+    ap.add_argument("--f32_exact_u8", default=None, choices=["true", "false"],
+                    help="serve an f32 request on the uint8 path when its values are exactly x/127.5-1 of "
+                         "8-bit pixels (the reference gateway's request); env KDL_F32_EXACT_U8 (default true)")
     ap.add_argument("--warm_signatures", default="",
                     help="comma list of signatures whose engines / graphs are built at model load (like "
                          "TF-Serving warmup requests); serving_default always is")
@@ -197,6 +201,7 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         exec_depth=a.exec_depth if a.exec_depth is not None else int(env.get("KDL_EXEC_DEPTH", "2")),
                         procs=max(1, a.procs), gpu_index=a.gpu_index,
                         warm_signatures=[s for s in a.warm_signatures.split(",") if s],
+                        f32_exact_u8=(a.f32_exact_u8 or env.get("KDL_F32_EXACT_U8", "true")).lower() != "false",
                         scatter=a.scatter, dp_world=a.dp_world, dp_rank=a.dp_rank, dp_signature=a.dp_signature,
                         log_format=a.log_format or env.get("KDL_LOG_FORMAT", "text"),
                         stats_log_interval_s=(a.stats_log_interval_s if a.stats_log_interval_s is not None

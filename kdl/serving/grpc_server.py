@@ -19,7 +19,7 @@ import numpy as np
 
 from ..ops import _lib
 from . import protos as P
-from .backend import ServingError
+from .backend import NATIVE_SIGNATURE, ServingError
 from .metrics import METRICS
 from .model_repo import ModelManager
 
@@ -104,8 +104,9 @@ def _image_payload(raw: bytes, td: dict, sig, dims: list) -> tuple[np.ndarray, i
 
 
 class Servicer:
-    def __init__(self, manager: ModelManager):
+    def __init__(self, manager: ModelManager, f32_exact_u8: bool = True):
         self.m = manager
+        self.f32_exact_u8 = f32_exact_u8
 
     # ---------------------------------------------------------------- Predict
     def predict(self, raw: bytes, context) -> bytes:
@@ -133,6 +134,14 @@ class Servicer:
                 if f != sig.output_key:
                     raise ServingError("INVALID_ARGUMENT", f"output tensor alias not found in signature: {f}")
             buf, n = _payload(raw, inputs[sig.input_key], sig)
+            if (self.f32_exact_u8 and sig.input_dtype == P.DT_FLOAT and sig.input_shape[1] > 0
+                    and NATIVE_SIGNATURE in s.signatures):
+                # the reference gateway's f32 request is exactly x / 127.5 - 1 of 8-bit pixels: serve it
+                # on the uint8 path (the same logits up to the stem's rounding of bf16(x) vs u8)
+                u8 = np.empty(n * sig.input_shape[1] * sig.input_shape[2] * 3, dtype=np.uint8)
+                if rt.f32_to_u8_exact(buf, u8):
+                    runner, buf = s.runner(NATIVE_SIGNATURE), u8
+                    METRICS.inc("kdl_f32_as_uint8_total")
             t1 = time.perf_counter()
             logits = runner.predict(buf, n, _deadline_us(context))
             t2 = time.perf_counter()
@@ -226,8 +235,9 @@ def signature_def_map(s) -> "P.SignatureDefMap":
     return m
 
 
-def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: int = 64, reuse_port: bool = False):
-    sv = Servicer(manager)
+def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: int = 64, reuse_port: bool = False,
+                      f32_exact_u8: bool = True):
+    sv = Servicer(manager, f32_exact_u8)
     raw = dict(request_deserializer=None, response_serializer=None)
     pred = grpc.method_handlers_generic_handler("tensorflow.serving.PredictionService", {
         "Predict": grpc.unary_unary_rpc_method_handler(sv.predict, **raw),

@@ -37,7 +37,7 @@ class ModelServer:
         # serve health/status immediately; Predict returns UNAVAILABLE until loaded
         reuse = cfg.gpu_index >= 0           # a child of the --procs launcher: ports are shared
         self.grpc, self.grpc_port, _ = build_grpc_server(self.manager, cfg.host, cfg.port, cfg.grpc_max_threads,
-                                                         reuse_port=reuse)
+                                                         reuse_port=reuse, f32_exact_u8=cfg.f32_exact_u8)
         self.grpc.start()
         if cfg.rest_api_port:
             self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port, reuse_port=reuse)

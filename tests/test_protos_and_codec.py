@@ -76,3 +76,20 @@ def test_model_spec_request_parse():
     req.model_spec.name = "m"
     req.model_spec.version.value = 7
     assert rt.parse_model_spec_request(req.SerializeToString())["version"] == 7
+
+
+def test_f32_to_u8_exact_detects_reference_preprocessing():
+    """kdl._rt.f32_to_u8_exact: the reference gateway's x = u8 / 127.5 - 1 (float32, keras_image_helper,
+    model_server.py:18) maps back to the exact pixels; any other float fails the check."""
+    import numpy as np
+    from kdl.ops import _lib
+    rt = _lib.rt()
+    u = np.random.default_rng(0).integers(0, 256, (2, 299, 299, 3), dtype=np.uint8)
+    u[0, 0, 0] = (0, 255, 128)
+    x = u.astype(np.float32) / 127.5 - 1
+    out = np.empty(u.size, np.uint8)
+    assert rt.f32_to_u8_exact(x, out) and np.array_equal(out.reshape(u.shape), u)
+    for bad in (0.5, 1.0000001, -1.5, float("nan")):
+        y = x.copy()
+        y[1, 7, 9, 2] = bad
+        assert not rt.f32_to_u8_exact(y, out), bad

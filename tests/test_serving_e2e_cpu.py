@@ -237,3 +237,22 @@ def test_deadline_exceeded(channel):
     with pytest.raises(grpc.RpcError) as e:
         stub.Predict(make_request(x), timeout=0.001)
     assert e.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED
+
+
+def test_reference_f32_request_rides_the_uint8_path(channel, server):
+    """The reference gateway's f32 request (x / 127.5 - 1 of 8-bit pixels, model_server.py:36-42) is
+    recognised as exact 8-bit pixels and served by the serving_uint8 runner: same logits as sending
+    the pixels, the f32 runner not involved; a non-pixel f32 request keeps the f32 path."""
+    from kdl.serving.metrics import METRICS
+    stub = PredictionStub(channel)
+    u8 = np.random.default_rng(9).integers(0, 256, (2, 299, 299, 3), dtype=np.uint8)
+    key = "kdl_f32_as_uint8_total"
+    n0 = METRICS.snapshot()["counters"].get(key, 0)
+    r1 = stub.Predict(make_request(u8.astype(np.float32) / 127.5 - 1), timeout=20.0)
+    r2 = stub.Predict(make_request(u8, signature="serving_uint8", input_key="images"), timeout=20.0)
+    a1 = np.asarray(r1.outputs["dense_7"].float_val, np.float32)
+    assert np.array_equal(a1, np.asarray(r2.outputs["dense_7"].float_val, np.float32))
+    assert METRICS.snapshot()["counters"].get(key, 0) == n0 + 1
+    x = u8.astype(np.float32) / 127.5 - 1 + 1e-3          # not pixels: f32 path
+    stub.Predict(make_request(x), timeout=20.0)
+    assert METRICS.snapshot()["counters"].get(key, 0) == n0 + 1

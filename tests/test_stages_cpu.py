@@ -101,7 +101,7 @@ def _xception_engine(fused=()):
             self.device = torch.device("cpu")
             self.max_batch, self.buckets, self.steps, self.in_kind = 1, [1], [], "u8"
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
-            self.fused_blocks = set(fused)
+            self.fused_blocks = {b: None for b in fused}
 
     p = X.init_params(seed=0)
     e = Fake(p)
