@@ -190,8 +190,13 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
     const bool last = s_last;
     __syncthreads();                          // every thread read the flag before the C tile reuses the LDS
     if (!last) return;                        // uniform: the whole workgroup leaves
+    // every split (this one included) stored its partial: sum them in split order, so the
+    // fp32 result does not depend on which split arrived last (bit-identical replays)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     for (int sp = 0; sp < S; ++sp) {
-      if (sp == ksid) continue;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll

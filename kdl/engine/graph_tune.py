@@ -17,7 +17,7 @@ the incumbent only if it wins an interleaved A/B re-measurement (``confirm``
 rounds, median) by more than ``margin``. One pass is ~N_variants graph captures.
 
     python -m kdl.engine.graph_tune --model xception --batch 32 --lanes 2 \
-        --out kdl/tuning/xception_b32_l2.json
+        --out /tmp/xception_b32_tuned.json
 """
 from __future__ import annotations
 

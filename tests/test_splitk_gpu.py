@@ -59,10 +59,15 @@ def test_splitk_residual_epilogue_in_captured_graph():
     lay.emit(prog, x.data_ptr(), y.data_ptr(), Geometry(B, H, H, H, H), res=r.data_ptr(), cfg=splitk_id(4, 16))
     s = torch.cuda.Stream()
     prog.capture(s.cuda_stream)
+    first = None
     for _ in range(5):
         y.zero_()
         torch.cuda.synchronize()
         prog.launch(s.cuda_stream)
         s.synchronize()
         assert _rel(y, ref) < 4e-3
+        # the last split sums every partial in split order: replays are bit-identical
+        if first is None:
+            first = y.clone()
+        assert torch.equal(y, first)
     assert int(lay._splitk_bufs[1].abs().sum()) == 0      # every tile's counter reset by its last split
