@@ -168,6 +168,11 @@ PYBIND11_MODULE(_rt, m) {
       .def_readonly("tickets", &Batch::tickets)
       .def_readonly("first_item", &Batch::first_item)
       .def_readonly("n_items", &Batch::n_items)
+      .def_property_readonly("dev_src", [](const Batch& b) {
+        std::vector<uintptr_t> v;
+        for (auto p : b.dev_src) v.push_back(reinterpret_cast<uintptr_t>(p));
+        return v;
+      })
       .def_readonly("oldest_enqueue_us", &Batch::oldest_enqueue_us);
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
@@ -192,6 +197,12 @@ PYBIND11_MODULE(_rt, m) {
         const size_t need = size_t(n_items) * b.options().item_bytes;
         if (size_t(info.size) * size_t(info.itemsize) < need) throw std::invalid_argument("payload smaller than n_items*item_bytes");
         return b.submit(reinterpret_cast<const uint8_t*>(info.ptr), n_items, deadline_us);
+      })
+      // device-resident payload (an address in device memory, e.g. a GPU-resized image batch):
+      // only native executors whose backend has issue_dev can run such batches
+      .def("submit_device", [](DynamicBatcher& b, uintptr_t ptr, int n_items, int64_t deadline_us) {
+        if (!ptr) throw std::invalid_argument("null device payload");
+        return b.submit(reinterpret_cast<const uint8_t*>(ptr), n_items, deadline_us, true);
       })
       // `out` may be larger than the ticket's n_items*out_cols floats, never smaller: a short
       // buffer gets ST_ERROR and is left untouched (the C++ side checks the size it is given)
@@ -233,7 +244,8 @@ PYBIND11_MODULE(_rt, m) {
       .def(py::init<int, size_t, int, int, int64_t, int>(), py::arg("nslots"), py::arg("item_bytes"),
            py::arg("max_batch"), py::arg("out_cols"), py::arg("latency_us") = 0, py::arg("fail_every") = 0)
       .def("api_ptr", [](FakeBackend& f) { return reinterpret_cast<uintptr_t>(&f.api); })
-      .def_readonly("issued", &FakeBackend::issued);
+      .def_readonly("issued", &FakeBackend::issued)
+      .def_readonly("dev_pieces", &FakeBackend::dev_pieces);
   py::class_<Executor>(m, "Executor")
       // `backend`: any object with api_ptr() -> address of its kdl_exec_backend (kdl._C.HipExecBackend,
       // FakeBackend). The executor keeps the batcher, the backend and the group alive (keep_alive):

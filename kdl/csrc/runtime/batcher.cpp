@@ -87,7 +87,7 @@ int DynamicBatcher::bucket_for(int n) const {
   return n;
 }
 
-int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadline_us) {
+int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadline_us, bool device) {
   if (n_items <= 0 || n_items > opt_.max_batch_size) return -ST_ERROR;
   std::lock_guard<std::mutex> lk(mu_);
   if (shutdown_) return -ST_SHUTDOWN;
@@ -98,6 +98,7 @@ int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadlin
   auto r = std::make_shared<Req>();
   r->ticket = next_ticket_++;
   r->data = data;
+  r->device = device;
   r->n_items = n_items;
   r->enqueue_us = now_us();
   r->deadline_us = deadline_us;
@@ -187,7 +188,7 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
     }
     // greedily pack whole requests in FIFO order
     int n = 0;
-    b->tickets.clear(); b->first_item.clear(); b->n_items.clear();
+    b->tickets.clear(); b->first_item.clear(); b->n_items.clear(); b->dev_src.clear();
     b->oldest_enqueue_us = queue_.front()->enqueue_us;
     while (!queue_.empty() && n + queue_.front()->n_items <= opt_.max_batch_size) {
       auto r = queue_.front();
@@ -197,6 +198,7 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
       b->tickets.push_back(r->ticket);
       b->first_item.push_back(n);
       b->n_items.push_back(r->n_items);
+      b->dev_src.push_back(r->device ? r->data : nullptr);
       n += r->n_items;
       take.push_back(r);
     }
@@ -217,6 +219,7 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
     size_t total = 0;
     constexpr size_t kPiece = size_t(1) << 20;
     for (size_t i = 0; i < take.size(); ++i) {
+      if (take[i]->device) continue;         // copied on the device by the backend
       uint8_t* dst = staging + size_t(b->first_item[i]) * opt_.item_bytes;
       const uint8_t* src = take[i]->data;
       const size_t n = size_t(take[i]->n_items) * opt_.item_bytes;

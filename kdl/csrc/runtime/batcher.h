@@ -46,6 +46,9 @@ struct Batch {
   std::vector<int64_t> tickets;
   std::vector<int> first_item;               // offset of each ticket's items in the batch
   std::vector<int> n_items;
+  // per ticket: nullptr = the payload was copied into staging; else a DEVICE pointer the
+  // backend copies device-to-device into its input slot (kdl_exec_backend::issue_dev)
+  std::vector<const uint8_t*> dev_src;
   int64_t oldest_enqueue_us = 0;
   int64_t formed_us = 0;                     // batch formed (before the payload copy)
 };
@@ -90,8 +93,12 @@ class DynamicBatcher {
   ~DynamicBatcher();
 
   // Producer: returns a ticket (> 0) or -ST_QUEUE_FULL / -ST_SHUTDOWN / -ST_ERROR.
-  // `data` must stay valid until wait() returns for this ticket.
-  int64_t submit(const uint8_t* data, int n_items, int64_t deadline_us);
+  // `data` must stay valid until wait() returns for this ticket. `device`: `data` is device
+  // memory (e.g. an image the GPU resized): next_batch does not copy it, the batch lists it in
+  // dev_src and the executor's backend copies it on the device; it must then stay valid
+  // until the batch's device work is done, not only until wait() (deadline-expired tickets
+  // return early), so device payloads come from buffers that are recycled, never freed.
+  int64_t submit(const uint8_t* data, int n_items, int64_t deadline_us, bool device = false);
   // Blocks until the request completes or its deadline passes; copies
   // n_items*out_cols floats into `out`, which holds `out_floats` floats (a smaller
   // buffer is not written and the call returns ST_ERROR). Returns a BatchStatus.
@@ -114,6 +121,7 @@ class DynamicBatcher {
   struct Req {
     int64_t ticket;
     const uint8_t* data;
+    bool device = false;
     int n_items;
     int64_t enqueue_us, deadline_us;
     State state = QUEUED;

@@ -89,6 +89,7 @@ bool Executor::fail(Batch& b, BatchTrace& tr) {
 
 void Executor::loop() {
   std::deque<Pending> pending;
+  std::vector<kdl_dev_piece> pieces;
   int slot = 0;
   bool gave_up = false;
   while (!stop_.load() && !gave_up) {
@@ -112,7 +113,15 @@ void Executor::loop() {
         if (fail_left_ > 0) --fail_left_;
         rc = -1;                                            // injected fault
       } else {
-        rc = be_.issue(be_.ctx, slot, p.batch.bucket, p.batch.n_real);
+        pieces.clear();
+        for (size_t i = 0; i < p.batch.dev_src.size(); ++i)
+          if (p.batch.dev_src[i]) pieces.push_back({p.batch.first_item[i], p.batch.n_items[i], p.batch.dev_src[i]});
+        if (pieces.empty())
+          rc = be_.issue(be_.ctx, slot, p.batch.bucket, p.batch.n_real);
+        else if (be_.issue_dev)
+          rc = be_.issue_dev(be_.ctx, slot, p.batch.bucket, p.batch.n_real, pieces.data(), int(pieces.size()));
+        else
+          rc = -1;                                          // this backend takes host payloads only
       }
       if (rc != 0) {
         gave_up = fail(p.batch, p.tr);
@@ -177,6 +186,15 @@ int fake_issue(void* ctx, int slot, int bucket, int n_real) {
   return 0;
 }
 
+int fake_issue_dev(void* ctx, int slot, int bucket, int n_real, const kdl_dev_piece* pc, int np) {
+  auto* f = static_cast<FakeBackend*>(ctx);   // "device" memory is host memory here
+  for (int i = 0; i < np; ++i)
+    std::memcpy(f->staging[slot].data() + size_t(pc[i].row) * f->item_bytes, pc[i].src,
+                size_t(pc[i].n_items) * f->item_bytes);
+  ++f->dev_pieces;
+  return fake_issue(ctx, slot, bucket, n_real);
+}
+
 int fake_complete(void* ctx, int slot, const float** out, kdl_device_times* t) {
   auto* f = static_cast<FakeBackend*>(ctx);
   const int64_t wait = f->ready_at[slot] - now_us();
@@ -199,6 +217,7 @@ FakeBackend::FakeBackend(int nslots, size_t item_bytes_, int max_batch, int out_
   api.staging = fake_staging;
   api.issue = fake_issue;
   api.complete = fake_complete;
+  api.issue_dev = fake_issue_dev;
 }
 
 }  // namespace kdl

@@ -132,10 +132,10 @@ class Executor {
 
 // Fake device backend for CPU tests and the sanitizer stress binary: result row i of a
 // batch = {first byte of item i, +1, +2, ...}; `latency_us` of simulated device time per
-// batch; fail_every > 0 fails every n-th issue.
+// batch; fail_every > 0 fails every n-th issue. Its "device" items are host pointers.
 struct FakeBackend {
   FakeBackend(int nslots, size_t item_bytes, int max_batch, int out_cols, int64_t latency_us, int fail_every = 0);
-  kdl_exec_backend api;
+  kdl_exec_backend api{};
   std::vector<std::vector<uint8_t>> staging;
   std::vector<std::vector<float>> out;
   std::vector<int64_t> ready_at;
@@ -144,6 +144,7 @@ struct FakeBackend {
   int out_cols;
   int64_t latency_us;
   int fail_every, issued = 0;
+  int dev_pieces = 0;                        // issue_dev calls (device-resident items)
 };
 
 }  // namespace kdl

@@ -9,6 +9,9 @@ uint8_t* be_staging(void* ctx, int slot) { return static_cast<HipExecBackend*>(c
 int be_issue(void* ctx, int slot, int bucket, int n_real) {
   return static_cast<HipExecBackend*>(ctx)->issue(slot, bucket, n_real);
 }
+int be_issue_dev(void* ctx, int slot, int bucket, int n_real, const kdl_dev_piece* pc, int np) {
+  return static_cast<HipExecBackend*>(ctx)->issue_dev(slot, bucket, n_real, pc, np);
+}
 int be_complete(void* ctx, int slot, const float** out, kdl_device_times* t) {
   return static_cast<HipExecBackend*>(ctx)->complete(slot, out, t);
 }
@@ -48,6 +51,7 @@ HipExecBackend::HipExecBackend(int device, int nslots, size_t item_bytes, int ma
   api_.staging = be_staging;
   api_.issue = be_issue;
   api_.complete = be_complete;
+  api_.issue_dev = be_issue_dev;
 }
 
 HipExecBackend::~HipExecBackend() {
@@ -134,15 +138,38 @@ void* HipExecBackend::dev_out(int slot, int bucket) const {
 }
 
 int HipExecBackend::issue(int slot, int bucket, int n_real) {
+  return issue_dev(slot, bucket, n_real, nullptr, 0);
+}
+
+int HipExecBackend::issue_dev(int slot, int bucket, int n_real, const kdl_dev_piece* pieces, int npieces) {
   (void)n_real;                               // padding rows are computed and ignored
   if (slot < 0 || slot >= nslots_) return -1;
   auto it = recipes_.find(bucket);
   if (it == recipes_.end()) return -1;
-  Recipe& r = it->second;
+  uint8_t* din = static_cast<uint8_t*>(it->second.dev_in[slot]);
   KDL_TRY(hipSetDevice(device_));
   if (timing_) KDL_TRY(hipEventRecord(ev_h2d0_[slot], copy_));
-  KDL_TRY(hipMemcpyAsync(r.dev_in[slot], staging_[slot], item_bytes_ * bucket, hipMemcpyHostToDevice, copy_));
+  // host rows: H2D in contiguous runs between the (row-sorted) device pieces; device rows: D2D
+  // (hipMemcpyDefault: a piece resized on another GPU of the node comes over xGMI)
+  int row = 0;
+  for (int i = 0; i <= npieces; ++i) {
+    const int end = i < npieces ? pieces[i].row : bucket;
+    if (end < row || end > bucket) return -1;
+    if (end > row)
+      KDL_TRY(hipMemcpyAsync(din + item_bytes_ * row, staging_[slot] + item_bytes_ * row, item_bytes_ * (end - row),
+                             hipMemcpyHostToDevice, copy_));
+    if (i == npieces) break;
+    const int n = pieces[i].n_items;
+    if (n < 1 || end + n > bucket || !pieces[i].src) return -1;
+    KDL_TRY(hipMemcpyAsync(din + item_bytes_ * end, pieces[i].src, item_bytes_ * n, hipMemcpyDefault, copy_));
+    row = end + n;
+  }
   KDL_TRY(hipEventRecord(ev_h2d1_[slot], copy_));
+  return finish_issue(slot, bucket);
+}
+
+int HipExecBackend::finish_issue(int slot, int bucket) {
+  Recipe& r = recipes_.find(bucket)->second;
   hipStream_t last = nullptr;
   if (launch(slot, bucket, ev_h2d1_[slot], &last) != 0) return -1;
   if (timing_) KDL_TRY(hipEventRecord(ev_fw1_[slot], last));

@@ -6,7 +6,8 @@
 // cross-batch parity waits of kdl/engine/stages.py) -> logits D2H behind the last stage;
 // complete() waits for the slot's done event and reports H2D / forward / D2H device times
 // from HIP events. Every call is asynchronous except complete(); nothing allocates after
-// construction.
+// construction. issue_dev() takes batches with device-resident rows (serving_image requests
+// resized on the GPU straight into device memory: no host round trip).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,6 +38,9 @@ class HipExecBackend {
   uint8_t* staging(int slot) { return staging_[slot]; }
   const float* host_out(int slot) const { return out_[slot]; }
   int issue(int slot, int bucket, int n_real);
+  // issue() whose rows of `pieces` come from device memory (D2D on the copy stream; the
+  // host rows are H2D'd in contiguous runs around them)
+  int issue_dev(int slot, int bucket, int n_real, const kdl_dev_piece* pieces, int npieces);
   // the recipe of `bucket` alone (no copies): stage 0 waits `ready`; *last = the last stage's
   // stream (its work is queued behind the forward). For the data-parallel ranks (comm.cpp).
   int launch(int slot, int bucket, hipEvent_t ready, hipStream_t* last);
@@ -53,6 +57,7 @@ class HipExecBackend {
   int complete(int slot, const float** out, kdl_device_times* t);
 
  private:
+  int finish_issue(int slot, int bucket);      // recipe launch + D2H behind the copies
   struct Recipe {
     int K = 1;
     std::vector<hipStream_t> streams;

@@ -243,6 +243,8 @@ class _Executor(threading.Thread):
                 t0 = time.perf_counter()
                 METRICS.observe("kdl_stage_ms", (rt.now_us() - batch.oldest_enqueue_us) / 1e3, stage="queue_wait")
                 try:
+                    if any(batch.dev_src):
+                        raise RuntimeError("device-resident items need a native executor")
                     self.faults.before_batch(self.name)
                     handle = self.issue(batch.bucket, batch.n_real, slot)
                 except BaseException:  # noqa: BLE001 - fail the batch, keep serving
@@ -432,7 +434,10 @@ class GPUExecutor(_Executor):
         if r.batcher is None:                 # a data-parallel follower: no batcher, no executor thread
             return
         fail, delay_us = self.faults.native_args(self.name)
-        self.native = rt.Executor(r.batcher, self.wrap_backend(be), r.exec_group, name=self.name, eager=self.eager,
+        wrapped = self.wrap_backend(be)
+        # the HIP backend copies device-resident rows itself (issue_dev); a DP leader does not
+        self.takes_device_items = wrapped is be
+        self.native = rt.Executor(r.batcher, wrapped, r.exec_group, name=self.name, eager=self.eager,
                                   max_failures=self.max_failures, fail_batches=fail, delay_us=delay_us)
 
     def wrap_backend(self, be):
@@ -581,7 +586,7 @@ class SignatureRunner:
             self.buckets = [b * cfg.dp_world for b in self.buckets]
         self.max_batch = self.buckets[-1]
         S = source.input_size
-        item_bytes = S * S * 3 * (1 if sig.input_dtype == P.DT_UINT8 else 4)
+        item_bytes = self.item_bytes = S * S * 3 * (1 if sig.input_dtype == P.DT_UINT8 else 4)
         timeout = bp.batch_timeout_micros if cfg.enable_batching else 0
         self.batcher = _lib.rt().DynamicBatcher(max_batch_size=self.max_batch, batch_timeout_us=timeout,
                                                 max_enqueued_batches=bp.max_enqueued_batches,
@@ -617,30 +622,44 @@ class SignatureRunner:
 
     def predict(self, payload, n: int, deadline_us: int) -> np.ndarray:
         """payload: buffer of n items (uint8 or f32 images); returns f32 [n, classes]."""
+        mv = memoryview(payload).cast("B")
+        ib = self.item_bytes
+        return self._run(n, lambda s, k: (self.batcher.submit(mv[s * ib:(s + k) * ib], k, deadline_us),
+                                          mv[s * ib:(s + k) * ib]))
+
+    def takes_device_items(self) -> bool:
+        """Every executor is a native one whose backend copies device-resident rows itself
+        (HipExecBackend::issue_dev): predict_device() may be used."""
+        return bool(self.executors) and all(getattr(ex, "takes_device_items", False) for ex in self.executors)
+
+    def predict_device(self, ptr: int, n: int, deadline_us: int) -> np.ndarray:
+        """Like predict(), for n items already in device memory at address ``ptr``."""
+        if not self.takes_device_items():
+            raise ServingError("INTERNAL", f"signature {self.sig.name} has no executor for device-resident items")
+        ib = self.item_bytes
+        return self._run(n, lambda s, k: (self.batcher.submit_device(ptr + s * ib, k, deadline_us), None))
+
+    def _run(self, n: int, submit) -> np.ndarray:
         rt = _lib.rt()
         if not self.healthy():
             raise ServingError("UNAVAILABLE", f"no healthy device left for signature {self.sig.name}")
         ncls = self.source.classes
         out = np.empty((n, ncls), dtype=np.float32)
-        S = self.source.input_size
-        item_bytes = S * S * 3 * (1 if self.sig.input_dtype == P.DT_UINT8 else 4)
-        mv = memoryview(payload).cast("B")
         tickets = []
         for s in range(0, n, self.max_batch):
             k = min(self.max_batch, n - s)
-            chunk = mv[s * item_bytes:(s + k) * item_bytes]
-            t = self.batcher.submit(chunk, k, deadline_us)
+            t, keep = submit(s, k)
             if t < 0:
                 for ss, tt, _ in tickets:  # drain what was already queued, each into a buffer of its size
                     self.batcher.wait(tt, np.empty((min(self.max_batch, n - ss), ncls), np.float32))
                 raise ServingError("RESOURCE_EXHAUSTED" if -t == rt.ST_QUEUE_FULL else "UNAVAILABLE",
                                    f"batcher rejected request (status {-t})")
-            tickets.append((s, t, chunk))
+            tickets.append((s, t, keep))
         status = rt.ST_OK
-        for s, t, chunk in tickets:
+        for s, t, keep in tickets:
             buf = np.empty((min(self.max_batch, n - s), ncls), dtype=np.float32)
             st = self.batcher.wait(t, buf)
-            del chunk
+            del keep
             if st == rt.ST_OK:
                 out[s:s + buf.shape[0]] = buf
             elif status == rt.ST_OK:

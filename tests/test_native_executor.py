@@ -143,3 +143,52 @@ def test_stop_drains_in_flight_batches(nslots):
     assert not th.is_alive()
     assert all(results) and len(results) + len(errors) == 10
     assert all(err[1] in (rt.ST_SHUTDOWN, rt.ST_ERROR) for err in errors)
+
+
+def test_device_resident_items_ride_issue_dev_beside_host_rows():
+    """submit_device (serving_image rows the GPU resized) and host submits share batches: the
+    executor hands the device rows to the backend's issue_dev as pieces (the fake backend's
+    "device" memory is host memory) and every request still gets its own rows back."""
+    b = _batcher()
+    g = rt.ExecGroup()
+    f = rt.FakeBackend(nslots=2, item_bytes=ITEM, max_batch=MAXB, out_cols=COLS, latency_us=200)
+    ex = rt.Executor(b, f, g, name="fake-dev")
+    ex.start()
+    errors, results, keep = [], [], []
+
+    def client(seed, device):
+        rng = np.random.default_rng(seed)
+        for _ in range(40):
+            n = int(rng.integers(1, 4))
+            vals = rng.integers(0, 200, size=n).astype(np.uint8)
+            data = np.repeat(vals, ITEM).astype(np.uint8)
+            keep.append(data)
+            t = b.submit_device(data.ctypes.data, n, 0) if device else b.submit(data, n, 0)
+            out = np.zeros((n, COLS), np.float32)
+            if t < 0 or b.wait(t, out) != rt.ST_OK:
+                errors.append(seed)
+                continue
+            want = vals[:, None].astype(np.float32) + np.arange(COLS, dtype=np.float32)[None]
+            results.append(bool(np.array_equal(out, want)))
+
+    ths = [threading.Thread(target=client, args=(s, s % 2 == 0)) for s in range(6)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    ex.stop()
+    b.shutdown()
+    assert not errors and len(results) == 240 and all(results)
+    assert f.dev_pieces > 0
+
+
+def test_batch_lists_device_items_for_the_backend():
+    """Only native executors take device-resident rows; the batch fails instead of running on
+    whatever the staging held."""
+    b = _batcher()
+    data = np.full(ITEM, 7, np.uint8)
+    t = b.submit_device(data.ctypes.data, 1, 0)
+    batch = b.next_batch(0, 1000, True)
+    assert batch is not None and batch.dev_src == [data.ctypes.data]
+    b.finish(batch, 0, rt.ST_ERROR)
+    assert b.wait(t, np.zeros((1, COLS), np.float32)) == rt.ST_ERROR

@@ -60,6 +60,40 @@ def test_gpu_serving_image_resizes_on_device_exactly(gpu_server):
         assert a.size == 10 * n and np.array_equal(a, np.asarray(r2.outputs["dense_7"].float_val, np.float32))
     s = gpu_server.manager.get("clothing-model", None, None)
     assert s.runner("serving_image").resizer.device is not None, "resize ran on the CPU"
+    assert s.runner("serving_image").device_path, "resized images round-tripped through the host"
+
+
+def test_gpu_serving_image_device_rows_share_batches_with_host_rows(gpu_server):
+    """Concurrent serving_image (device-resident rows, D2D into the engine slot) and
+    serving_uint8 (pinned staging, H2D) requests land in the same batches; every request
+    gets the logits of its own PIL-resized images (up to the bucket graphs' bf16 rounding:
+    a batch of another size runs another captured graph)."""
+    import threading
+    from PIL import Image
+    s = gpu_server.manager.get("clothing-model", None, None)
+    img, u8 = s.runner("serving_image"), s.runner("serving_uint8")
+    rng = np.random.default_rng(3)
+    raws = [rng.integers(0, 256, (1 + i % 2, 300 + 37 * i, 400 - 23 * i, 3), dtype=np.uint8) for i in range(6)]
+    pils = [np.stack([np.asarray(Image.fromarray(im).resize((299, 299), Image.NEAREST)) for im in r]) for r in raws]
+    want = [u8.predict(p, p.shape[0], 0) for p in pils]
+    got, errs = {}, []
+
+    def worker(i):
+        try:
+            for _ in range(4):
+                got.setdefault(i, []).append(img.predict(raws[i], raws[i].shape[0], 0) if i % 2 == 0
+                                             else u8.predict(pils[i], pils[i].shape[0], 0))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs, errs
+    for i in range(6):
+        scale = np.abs(want[i]).max()
+        assert all(np.abs(g - want[i]).max() <= 0.02 * scale for g in got[i]), i
 
 
 def test_rccl_world1_dp_runner():
