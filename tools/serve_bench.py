@@ -95,7 +95,9 @@ def main(argv=None) -> int:
     ap.add_argument("--clients", type=int, default=32)
     ap.add_argument("--images", type=int, default=1)
     ap.add_argument("--seconds", type=float, default=15)
-    ap.add_argument("--signature", default="serving_uint8", choices=["serving_uint8", "serving_default"])
+    ap.add_argument("--signature", default="serving_uint8", choices=["serving_uint8", "serving_default", "serving_image"])
+    ap.add_argument("--image-size", default="534x400",
+                    help="serving_image: HxW of the raw uint8 images the clients send (resized on the server)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--max-batch", type=int, default=32)
     ap.add_argument("--timeout-us", type=int, default=1000)
@@ -120,13 +122,14 @@ def main(argv=None) -> int:
                          "process, which then share its GIL with the server's handlers)")
     a = ap.parse_args(argv)
     rng = np.random.default_rng(0)
-    u8 = rng.integers(0, 256, (a.images, 299, 299, 3), dtype=np.uint8)
+    H, W = (299, 299) if a.signature != "serving_image" else map(int, a.image_size.split("x"))
+    u8 = rng.integers(0, 256, (a.images, H, W, 3), dtype=np.uint8)
     procs = []
     if a.client_procs:
         import multiprocessing as mp
         from kdl.gateway.client import make_request as _mk
-        if a.signature == "serving_uint8":
-            req0 = _mk(u8, signature="serving_uint8", input_key="images").SerializeToString()
+        if a.signature != "serving_default":
+            req0 = _mk(u8, signature=a.signature, input_key="images").SerializeToString()
         else:
             req0 = _mk(u8.astype(np.float32) / 127.5 - 1).SerializeToString()
         ctx = mp.get_context("spawn")         # before any GPU initialisation in this process
@@ -162,8 +165,8 @@ def main(argv=None) -> int:
         if a.signature != "serving_default":
             srv.manager.get("clothing-model").runner(a.signature)
         target = f"127.0.0.1:{srv.grpc_port}"
-    if a.signature == "serving_uint8":
-        req = make_request(u8, signature="serving_uint8", input_key="images").SerializeToString()
+    if a.signature != "serving_default":
+        req = make_request(u8, signature=a.signature, input_key="images").SerializeToString()
     else:
         req = make_request(u8.astype(np.float32) / 127.5 - 1).SerializeToString()
     lat, lock = [], threading.Lock()
@@ -201,6 +204,10 @@ def main(argv=None) -> int:
            "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2)}
     if srv is not None:
         run = srv.manager.get("clothing-model").runner(a.signature)
+        if a.signature == "serving_image":
+            res["image_size"] = a.image_size
+            res["resize_into_device_slot"] = bool(getattr(run, "device_path", False))
+        run = getattr(run, "inner", run)      # serving_image: the serving_uint8 runner behind the resize
         st = run.batcher.stats()
         res["mean_batch"] = round(st["items"] / max(1, st["batches"]), 2)
         if a.stages:
