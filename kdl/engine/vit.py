@@ -69,8 +69,11 @@ class ViTEngine(EngineBase):
         # residual as its C operand); not for mlp.0 (hipBLASLt's GELU epilogue measured 64.2 vs
         # 58.4 us for our exact-erf one, profiles/vit_blaslt_r3.txt) or the patch embedding
         # (writes into per-image token rows)
+        # split-K candidates: N = 768 outputs (out_proj, mlp.3) are 120 tiles of 160 x 256 at the
+        # bench's 6,304 token rows, under half of the 256 CUs; 2-4 splits fill the chip
         lay = ConvGemmLayer(name, MODE_PW, w.double(), b.float(), cin_pad=w.shape[1], n=w.shape[0],
-                            relu_out=relu_out, device=self.device, blaslt=blaslt and relu_out != 3)
+                            relu_out=relu_out, device=self.device, blaslt=blaslt and relu_out != 3,
+                            ksplit=(2, 3, 4) if w.shape[0] <= 768 and w.shape[1] % 384 == 0 else ())
         lay.krot = 1    # K-rotated LDS-DMA GEMM: bf16 +0.6 % img/s, p50 -2.9 % (profiles/krot_ab.txt)
         return lay
 

@@ -192,7 +192,7 @@ class ConvGemmLayer:
                  blaslt: bool = False, ksplit: tuple = ()):
         """``dtype``: element type of the activations and packed weights, bf16 (default)
         or fp16 (MODE_PW / MODE_CONV only; ``dt`` = 1 in the launch args).
-        ``ksplit``: split-K factors to offer with the LDS-DMA GEMM tiles of at most 128 rows
+        ``ksplit``: split-K factors to offer with the LDS-DMA GEMM tiles of at most 160 rows
         (ids >= SPLITK_BASE; for layers whose M fills few CUs: ResNet-50 layer3/4).
         ``blaslt``: also offer the hipBLASLt GEMM node (ids >= BLT_BASE) as a variant; only
         for a plain stride-1 pointwise linear whose epilogue is bias (+ReLU) (+residual
@@ -241,7 +241,7 @@ class ConvGemmLayer:
         """(split, cfg) pairs valid for this layer (``W``: image width, filters the
         fused separable configs whose LDS row band would not fit)."""
         skv = [(False, splitk_id(sk, c)) for sk in self.ksplit for c in self.candidates
-               if PIPE_BASE <= c < SEP_BASE and cfg_tile(c)[0] <= 128 and (self.K // 32) % sk == 0]
+               if PIPE_BASE <= c < SEP_BASE and cfg_tile(c)[0] <= 160 and (self.K // 32) % sk == 0]
         if self.mode == MODE_CONV:
             return [(False, c) for c in self.candidates
                     if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))] + skv

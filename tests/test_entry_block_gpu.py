@@ -37,7 +37,9 @@ def _layers(p, blk):
 GEOM = {2: (147, 64, 74, 128), 3: (74, 128, 37, 256)}
 
 
-CASES = [(2, 2, None), (2, 2, 5), (2, 3, 97), (2, 1, 1), (3, 2, None), (3, 3, 7), (3, 1, 1)]
+# (block, batch, grid): grids small enough that workgroups run many pooled rows, but whose step
+# lists still fit the kernel's LDS step table (EB_MAX_STEPS)
+CASES = [(2, 2, None), (2, 2, 9), (2, 3, 97), (2, 1, 8), (3, 2, None), (3, 3, 7), (3, 1, 1)]
 # kernel configs per block (entry_block.hip KDL_EB_CONFIGS): VALU / MFMA depthwise, 1 or 2 WGs per CU
 BLOCK_CFGS = {2: [0, 2, 4, 5], 3: [1]}
 
@@ -63,6 +65,14 @@ def test_entry_block_matches_oracle(xparams, blk, B, grid, cfg):
     err = ((got - ref).abs().max() / ref.abs().max()).item()
     print(f"entry block{blk} B={B} grid={grid} cfg {cfg}: rel max err {err:.2e}")
     assert err < 2e-2, err
+
+
+def test_entry_block_refuses_a_step_table_over_the_lds_limit(xparams):
+    from kdl.ops.entry_block import EntryBlock
+    s1, s2, r = _layers(xparams, 2)
+    eb = EntryBlock("block2", s1, s2, r, device=DEV, grid=1)
+    with pytest.raises(AssertionError, match="EB_MAX_STEPS"):
+        eb.plan(2, 74, 74)
 
 
 def test_entry_block2_replays_bit_identical(xparams):
