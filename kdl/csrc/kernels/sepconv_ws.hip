@@ -406,7 +406,7 @@ struct WideGeom {
   static_assert(FM % 2 == 0, "units");
 };
 
-template <int FM, int FN, int XB, bool RELU>
+template <int FM, int FN, int XB, bool RELU, bool KROT>
 __global__ __launch_bounds__(512) void sepconv_wide_kernel(ConvGemmArgs a) {
   using G = WideGeom<FM, FN, XB, RELU>;
   constexpr int BM = G::BM, BN = G::BN, L = G::L, NDMA = G::NDMA, STAGE = G::STAGE;
@@ -428,7 +428,13 @@ __global__ __launch_bounds__(512) void sepconv_wide_kernel(ConvGemmArgs a) {
   const int KT = a.K >> 5;
   const long P0 = (long)m0 - W - 1;
   const int NS = min(m0 + BM, a.M) - m0 + 2 * W + 2;
-  auto kc = [&](int t) { return t < KT ? t : KT - 1; };
+  // KROT: each M tile walks K from its own start (sepconv_ws KROT): the workgroups do not all
+  // fetch the same weight fragments at the same time
+  const int krot = KROT ? (mi * 7) % KT : 0;
+  auto kc = [&](int t) {
+    t = (t < KT ? t : KT - 1) + krot;
+    return t >= KT ? t - KT : t;
+  };
 
   // ---- DMA sources of this wave's L pieces (piece index s = wave + 8 i, uniform per wave)
   const uint8_t* dsrc[L];
@@ -620,12 +626,15 @@ __global__ __launch_bounds__(512) void sepconv_wide_kernel(ConvGemmArgs a) {
   X(27, 6, 6, 5, 9)
 
 // wide-tile kernel (sepconv_wide_kernel): (id, FM, FN, XB): tile 32*FM x 64*FN, 8 waves as a
-// 2 x 4 grid of FM x FN fragments, 3-slot ring of (XB + 1 + 4*FN) KiB stages
+// 2 x 4 grid of FM x FN fragments, 3-slot ring of (XB + 1 + 4*FN) KiB stages; ids 34, 35 = 30,
+// 31 walking K from a per-M-tile rotated start
 #define KDL_SEPWIDE_CONFIGS(X) \
   X(30, 6, 6, 15)             \
   X(31, 6, 4, 15)             \
   X(32, 8, 4, 19)             \
-  X(33, 4, 6, 11)
+  X(33, 4, 6, 11)             \
+  X(34, 6, 6, 15)             \
+  X(35, 6, 4, 15)
 
 // id 7: s_memtime stamping variant (tools/stamps.py; never tuned); ids 23-26 = 0, 2, 3, 5
 // walking K from a per-M-tile rotated start
@@ -690,9 +699,9 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
 #define KDL_WIDECASE(id, fm, fn, xb)                                                                 \
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_wide_kernel<fm, fn, xb, true>), dim3(grid), dim3(th), 0, s, a);    \
+      hipLaunchKernelGGL((sepconv_wide_kernel<fm, fn, xb, true, (id >= 34)>), dim3(grid), dim3(th), 0, s, a);  \
     else                                                                                            \
-      hipLaunchKernelGGL((sepconv_wide_kernel<fm, fn, xb, false>), dim3(grid), dim3(th), 0, s, a);   \
+      hipLaunchKernelGGL((sepconv_wide_kernel<fm, fn, xb, false, (id >= 34)>), dim3(grid), dim3(th), 0, s, a); \
     break;
     KDL_SEPWIDE_CONFIGS(KDL_WIDECASE)
 #undef KDL_WIDECASE
