@@ -365,239 +365,6 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, ABL>(a, wg / nN, wg % nN, smem);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Wide-tile variant: every wave is producer AND consumer, all operands by
-// LDS-DMA. The warp-specialized tile above streams 34 KB per k-step into a CU for 96 x 384
-// outputs (70 % of it pointwise weights) and waits at the barrier 40-55 % of each step for
-// them; its tile is capped by the consumers' registers (4 of the 8 waves hold accumulators).
-// Here all 8 waves hold accumulators (2 x 4 wave grid, FM x FN fragments each), so the tile
-// is 32*FM x 64*FN: at 192 x 384 a k-step brings 40 KB for twice the outputs (-41 % bytes per
-// FLOP). Per k-step t every wave
-//   * LDS-DMAs its L = ceil(NDMA / 8) 1 KiB pieces of stage t+2 (stage s = band(s+1), depthwise
-//     entries(s+1), pointwise weights(s): each stage is consumed by exactly one step, so a
-//     3-slot ring keeps two stages in flight);
-//   * computes its 3 depthwise units (16 px x 16 ch, 5 block-diagonal MFMAs each, the
-//     sepconv_ws producer math) of k-step t+1 into A[(t+1)&1];
-//   * multiplies A[t&1] (its FM row fragments) by the stage's weights (its FN column
-//     fragments): FM*FN MFMAs.
-// One counted vmcnt(L) + lgkmcnt(0) + barrier per step publishes stage t and A[t&1].
-// vmcnt(N) + lgkmcnt(0) + barrier: this wave's DMAs up to the N youngest have landed and its
-// LDS writes (the A buffer) are done before anybody passes
-template <int N>
-__device__ __forceinline__ void wide_wait_barrier() {
-  static_assert(N < 64, "vmcnt is 6 bits");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
-  __builtin_amdgcn_s_barrier();
-}
-
-template <int FM, int FN, int XB, bool RELU>
-struct WideGeom {
-  static constexpr int BM = 32 * FM, BN = 64 * FN;
-  static constexpr int BF = BN / 16;               // pointwise weight fragments per k-step
-  static constexpr int NDMA = XB + 1 + BF;         // 1 KiB pieces per stage
-  static constexpr int L = (NDMA + 7) / 8;         // per wave per stage (surplus re-issues)
-  static constexpr int STAGE = NDMA * 1024;
-  static constexpr int RING = 3 * STAGE;
-  static constexpr int ABUF = 2 * FM * 1024;       // BM rows x 32 k of bf16
-  static constexpr int PIPE = RING + 2 * ABUF;
-  static constexpr int CS = BN * 2 + 16;
-  static constexpr int BYTES = PIPE > BM * CS ? PIPE : BM * CS;
-  static_assert(BYTES <= 160 * 1024, "LDS");
-  static_assert(FM % 2 == 0, "units");
-};
-
-template <int FM, int FN, int XB, bool RELU, bool KROT>
-__global__ __launch_bounds__(512) void sepconv_wide_kernel(ConvGemmArgs a) {
-  using G = WideGeom<FM, FN, XB, RELU>;
-  constexpr int BM = G::BM, BN = G::BN, L = G::L, NDMA = G::NDMA, STAGE = G::STAGE;
-  constexpr int NSP = 16 * XB, PL = NSP * 16, ZSLOT = NSP - 1;
-  constexpr int UPW = FM / 2;                     // depthwise units per wave: 2*(BM/16) units / 8 waves
-  static_assert(UPW * 8 == 2 * (BM / 16), "unit split");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[G::BYTES];
-
-  const int nN = (a.NF * 16) / BN;
-  const int nM = (a.M + BM - 1) / BM;
-  const int wg = xcd_remap(blockIdx.x, nM * nN);
-  const int mi = wg / nN, ni = wg % nN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int W = a.W, H = a.H;
-  const long NPIX = (long)a.B * H * W;
-  const int m0 = mi * BM, n0 = ni * BN;
-  const int KT = a.K >> 5;
-  const long P0 = (long)m0 - W - 1;
-  const int NS = min(m0 + BM, a.M) - m0 + 2 * W + 2;
-  // KROT: each M tile walks K from its own start (sepconv_ws KROT): the workgroups do not all
-  // fetch the same weight fragments at the same time
-  const int krot = KROT ? (mi * 7) % KT : 0;
-  auto kc = [&](int t) {
-    t = (t < KT ? t : KT - 1) + krot;
-    return t >= KT ? t - KT : t;
-  };
-
-  // ---- DMA sources of this wave's L pieces (piece index s = wave + 8 i, uniform per wave)
-  const uint8_t* dsrc[L];
-  int dkind[L], doff[L];                            // 0 band (k-step of s+1), 1 dw entries (s+1), 2 weights (s)
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-    const int s = min(wave + 8 * i, NDMA - 1);
-    doff[i] = s * 1024;
-    if (s < XB) {
-      const int c = s * 64 + lane;
-      const int q = c / NSP, slot = c - q * NSP;
-      long p = P0 + slot;
-      p = p < 0 ? 0 : (p >= NPIX ? NPIX - 1 : p);
-      dsrc[i] = slot < NS ? (const uint8_t*)(a.x + p * a.ldx + q * 8) : sepw_zeros;
-      dkind[i] = 0;
-    } else if (s == XB) {
-      dsrc[i] = (const uint8_t*)a.dwk + lane * 16;
-      dkind[i] = 1;
-    } else {
-      dsrc[i] = (const uint8_t*)(a.wp + ((long)(n0 / 16 + (s - XB - 1)) * KT) * 512 + lane * 8);
-      dkind[i] = 2;
-    }
-  }
-  auto issue = [&](int st, int slot) {             // stage st: band / entries of k-step st+1, weights of st
-    uint8_t* base = smem + slot * STAGE;
-    const int kx = kc(st + 1), kw = kc(st);
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-      long o;
-      if (dkind[i] == 0) o = (long)kx * 64;                      // 32 channels of the k-step
-      else if (dkind[i] == 1) o = (long)kx * 1024;
-      else o = (long)kw * 1024;
-      glds16(dsrc[i] + o, base + doff[i]);
-    }
-  };
-  // stage -1 carries band(0) / entries(0) for the first depthwise
-  auto issue_pre = [&](int slot) {
-    uint8_t* base = smem + slot * STAGE;
-#pragma unroll
-    for (int i = 0; i < L; ++i) glds16(dsrc[i], base + doff[i]);
-  };
-
-  // ---- depthwise geometry: units u = wave + 8 i -> row fragment u >> 1, channel group wave & 1
-  const int g = wave & 1;
-  const int p16 = lane & 15, kb = lane >> 4;
-  const int par = kb >> 1, qc = 2 * g + (kb & 1);
-  int toff[UPW][5];
-#pragma unroll
-  for (int i = 0; i < UPW; ++i) {
-    const int u = wave + 8 * i;
-    int mg = m0 + (u >> 1) * 16 + p16;
-    mg = mg < a.M ? mg : a.M - 1;
-    const int R = mg / W, w = mg - R * W, h = R % H;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const int tap = 2 * j + par;
-      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-      const bool ok = tap < 9 && (unsigned)(h + dy) < (unsigned)H && (unsigned)(w + dx) < (unsigned)W;
-      const int slot = ok ? (int)(mg + dy * W + dx - P0) : ZSLOT;
-      toff[i][j] = qc * PL + slot * 16;
-    }
-  }
-  const bool wv = (p16 >> 3) == (kb & 1);
-  const int e = p16 & 7;
-  uint32_t sel[2][4];
-#pragma unroll
-  for (int jp = 0; jp < 2; ++jp)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t pair = (2u * jp) | ((2u * jp + 1u) << 8);
-      const uint32_t val = (e & 1) ? (0x0c0cu | (pair << 16)) : (0x0c0c0000u | pair);
-      sel[jp][d] = (wv && (e >> 1) == d) ? val : 0x0c0c0c0cu;
-    }
-  const int went = XB * 1024 + ((g * 16 + p16) * 2 + par) * 16;
-  const int aoffw = (p16 + 16 * (2 * g + (kb >> 1))) * 16 + 8 * (kb & 1);
-
-  // depthwise of the band in ring slot `slot` into A buffer `abuf`
-  auto dw = [&](int slot, int abuf) {
-    const uint8_t* sb = smem + slot * STAGE;
-    const u32x4 we = *(const u32x4*)(sb + went);
-    s16x8 wf[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const uint32_t wd = we[j >> 1];
-      u32x4 f;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) f[d] = __builtin_amdgcn_perm(wd, wd, sel[j & 1][d]);
-      wf[j] = __builtin_bit_cast(s16x8, f);
-    }
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-      f32x4 dacc = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        u32x4 v = *(const u32x4*)(sb + toff[i][j]);
-        if constexpr (RELU) {
-#pragma unroll
-          for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
-        }
-        dacc = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc);
-      }
-      const u32x2 o = {pack_bf16(dacc[0], dacc[1]), pack_bf16(dacc[2], dacc[3])};
-      *(u32x2*)(smem + G::RING + abuf * G::ABUF + ((wave + 8 * i) >> 1) * 1024 + aoffw) = o;
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  issue_pre(2);
-  issue(0, 0);
-  issue(1, 1);
-  wide_wait_barrier<2 * L>();
-  dw(2, 0);
-  for (int t = 0; t < KT; ++t) {
-    wide_wait_barrier<L>();    // stage t landed, A[t&1] written
-    const int sl = t % 3;
-    issue(t + 2, (t + 2) % 3);
-    dw(sl, (t + 1) & 1);                              // k-step t+1 (a clamped repeat past the end)
-    const uint8_t* As = smem + G::RING + (t & 1) * G::ABUF + (wm * FM) * 1024 + lane * 16;
-    const uint8_t* Bs = smem + sl * STAGE + (XB + 1 + wn * FN) * 1024 + lane * 16;
-    s16x8 af[FM];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(As + i * 1024);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const s16x8 bf = *(const s16x8*)(Bs + j * 1024);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) acc[i][j] = mfma16(bf, af[i], acc[i][j]);
-    }
-  }
-  wide_wait_barrier<0>();
-
-  // ---- epilogue: bias (+ReLU) -> bf16 C tile in LDS -> (+residual) 16-byte stores
-  constexpr int CS = G::CS;
-  const int quad = lane >> 4, col = lane & 15;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int nl = wn * FN * 16 + j * 16 + 4 * quad;
-    const float4 bv = *(const float4*)(a.bias + n0 + nl);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int mll = (wm * FM + i) * 16 + col;
-      float v0 = acc[i][j][0] + bv.x, v1 = acc[i][j][1] + bv.y;
-      float v2 = acc[i][j][2] + bv.z, v3 = acc[i][j][3] + bv.w;
-      if (a.relu_out == 1) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      *(u32x2*)(smem + mll * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
-    }
-  }
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  for (int c = tid; c < BM * CPR; c += 512) {
-    const int r = c / CPR, cc = c - r * CPR;
-    const int m = m0 + r, n = n0 + cc * 8;
-    if (m < a.M && n < a.nstore) epi_store(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
-  }
-}
-
 // (FM, FN, STAGES, XB = band KiB): tile BM = 16*FM, BN = 64*FN; LDS = STAGES*(XB+1) KiB + 2FM KiB
 // (+ the BM x BN bf16 C tile, which reuses it); the band needs BM + 2W + 3 <= 16*XB.
 // Retired ids (round 3): 8-14, 18, 19, 27 were timing ablations (no depthwise / pointwise MFMA,
@@ -625,17 +392,6 @@ __global__ __launch_bounds__(512) void sepconv_wide_kernel(ConvGemmArgs a) {
   X(26, 4, 6, 5, 8)          \
   X(27, 6, 6, 5, 9)
 
-// wide-tile kernel (sepconv_wide_kernel): (id, FM, FN, XB): tile 32*FM x 64*FN, 8 waves as a
-// 2 x 4 grid of FM x FN fragments, 3-slot ring of (XB + 1 + 4*FN) KiB stages; ids 34, 35 = 30,
-// 31 walking K from a per-M-tile rotated start
-#define KDL_SEPWIDE_CONFIGS(X) \
-  X(30, 6, 6, 15)             \
-  X(31, 6, 4, 15)             \
-  X(32, 8, 4, 19)             \
-  X(33, 4, 6, 11)             \
-  X(34, 6, 6, 15)             \
-  X(35, 6, 4, 15)
-
 // id 7: s_memtime stamping variant (tools/stamps.py; never tuned); ids 23-26 = 0, 2, 3, 5
 // walking K from a per-M-tile rotated start
 constexpr bool sepw_stamp(int id) { return id == 7; }
@@ -646,10 +402,6 @@ static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * x
 
 int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads) {
   switch (cfg) {
-#define KDL_WIDEINFO(id, fm, fn, xb) \
-  case id: *bm = 32 * fm; *bn = 64 * fn; *threads = 512; return 0;
-    KDL_SEPWIDE_CONFIGS(KDL_WIDEINFO)
-#undef KDL_WIDEINFO
 #define KDL_SWINFO(id, fm, fn, st, xb) \
   case id: *bm = 16 * fm; *bn = 64 * fn; *threads = 512; return 0;
     KDL_SEPW_CONFIGS(KDL_SWINFO)
@@ -660,10 +412,6 @@ int sepconv_ws_config(int cfg, int* bm, int* bn, int* threads) {
 
 int sepconv_ws_fits(int cfg, int W) {
   switch (cfg) {
-#define KDL_WIDEFIT(id, fm, fn, xb) \
-  case id: return sepw_fits_xb(32 * fm, W, xb);
-    KDL_SEPWIDE_CONFIGS(KDL_WIDEFIT)
-#undef KDL_WIDEFIT
 #define KDL_SWFIT(id, fm, fn, st, xb) \
   case id: return sepw_fits_xb(16 * fm, W, xb);
     KDL_SEPW_CONFIGS(KDL_SWFIT)
@@ -696,15 +444,6 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)
 #undef KDL_SWCASE
-#define KDL_WIDECASE(id, fm, fn, xb)                                                                 \
-  case id:                                                                                          \
-    if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_wide_kernel<fm, fn, xb, true, (id >= 34)>), dim3(grid), dim3(th), 0, s, a);  \
-    else                                                                                            \
-      hipLaunchKernelGGL((sepconv_wide_kernel<fm, fn, xb, false, (id >= 34)>), dim3(grid), dim3(th), 0, s, a); \
-    break;
-    KDL_SEPWIDE_CONFIGS(KDL_WIDECASE)
-#undef KDL_WIDECASE
   }
   return hipGetLastError();
 }

@@ -45,9 +45,7 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            143: (6, 6, 1, 4), 144: (6, 6, 1, 4), 145: (6, 6, 1, 4), 146: (4, 6, 1, 4),
            # timing ablation of 143 (sepconv_ws.hip ABL; wrong values): full-line band reads
            147: (6, 6, 1, 4),
-           # wide tiles, every wave producer and consumer (sepconv_ws.hip KDL_SEPWIDE_CONFIGS): (FM, FN, 2, 4)
-           150: (6, 6, 2, 4), 151: (6, 4, 2, 4), 152: (8, 4, 2, 4), 153: (4, 6, 2, 4),
-           154: (6, 6, 2, 4), 155: (6, 4, 2, 4),   # = 150, 151 with K rotated per M tile
+           # 150-155: round 4's wide-tile variant, measured 1.5-2.2x slower and removed (profiles/sepconv_wide_r4.txt)
            # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
            160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
            165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
@@ -75,7 +73,7 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 # x-band KiB per stage of each KDL_SEPW_CONFIGS entry (mirror of sepconv_ws_fits)
 SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
            135: 15, 136: 11, 137: 15, 140: 8, 141: 8, 142: 8,
-           143: 9, 144: 11, 145: 16, 146: 8, 147: 9, 150: 15, 151: 15, 152: 19, 153: 11, 154: 15, 155: 15}
+           143: 9, 144: 11, 145: 16, 146: 8, 147: 9}
 # ids >= BLT_BASE: the vendor GEMM node (hipBLASLt, runtime/blaslt.cpp) for plain dense linears of
 # layers built with blaslt=True; id - BLT_BASE = rank in hipBLASLt's heuristic list for the shape
 BLT_BASE = 1000

@@ -62,7 +62,7 @@ def test_splitk_ids_variants_and_tuning():
     lay = ConvGemmLayer("c2", MODE_CONV, torch.randn(256, 9 * 256, generator=g, dtype=torch.float64),
                         torch.randn(256, generator=g), cin_pad=256, n=256, device="cpu", ksplit=(2, 3))
     sk = [c for _, c in lay.variants(14) if is_splitk(c)]
-    assert sk and all(splitk_parts(c)[0] in (2, 3) and cfg_tile(c)[0] <= 128 for c in sk)
+    assert sk and all(splitk_parts(c)[0] in (2, 3) and cfg_tile(c)[0] <= 160 for c in sk)
     assert splitk_parts(splitk_id(3, 16)) == (3, 16) and not is_blaslt(splitk_id(3, 16))
     plain = _lin()                                             # built without ksplit: refused
     eng = _Eng([lay, plain])
