@@ -115,6 +115,8 @@ def main(argv=None) -> int:
                     help="rccl: serve from `python -m kdl.serving --scatter rccl --dp_world W` (one front-end, "
                          "the native RCCL data-parallel executor, serving/dp.py)")
     ap.add_argument("--dp-world", type=int, default=1)
+    ap.add_argument("--no-f32-exact", action="store_true",
+                    help="in-process server: f32 requests that are exact 8-bit pixels are NOT moved to the uint8 path")
     ap.add_argument("--stages", action="store_true",
                     help="in-process server: print the native executor's mean per-stage times")
     ap.add_argument("--client-procs", type=int, default=0,
@@ -159,6 +161,7 @@ def main(argv=None) -> int:
         cfg = ServerConfig(port=0, rest_api_port=0, model_base_path=base, device=a.device, gpus=a.gpus,
                            executors_per_gpu=a.executors_per_gpu,
                            host="127.0.0.1", file_system_poll_wait_seconds=0, grpc_max_threads=max(64, a.clients * 2),
+                           f32_exact_u8=not a.no_f32_exact,
                            batching=BatchingParams(max_batch_size=a.max_batch, batch_timeout_micros=a.timeout_us,
                                                    allowed_batch_sizes=sizes, eager_when_idle=not a.no_eager))
         srv = ModelServer(cfg).start(block_until_loaded=True)
@@ -203,6 +206,7 @@ def main(argv=None) -> int:
            "p50_ms": round(statistics.median(lat) * 1e3, 2),
            "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2)}
     if srv is not None:
+        res["f32_exact_u8"] = not a.no_f32_exact
         run = srv.manager.get("clothing-model").runner(a.signature)
         if a.signature == "serving_image":
             res["image_size"] = a.image_size
