@@ -178,9 +178,14 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
   X(12, 5, 2, 2, 4, 3)     \
   X(13, 4, 2, 2, 4, 3)     \
   X(14, 5, 2, 2, 4, 4)     \
-  X(15, 4, 2, 2, 4, 4)
+  X(15, 4, 2, 2, 4, 4)     \
+  X(16, 8, 4, 2, 4, 2)     \
+  X(17, 6, 4, 2, 4, 2)
 // 8-10: 160-row tiles, whole waves of 256 CUs at the ViT-B/16 token count (gemm_pipe.hip 45-47);
 // 11-15: 3-4 stage rings of the large tiles (2 stages leave one k-step of load latency exposed)
+// 16-17: 256 x 256 / 192 x 256 tiles: at 128-deep fp8 k-steps a 160 x 128 tile needs ~57 B/clk per CU
+// to keep the MFMAs busy, more than an L2-fed CU takes in (~28-30); 256 x 256 needs ~32 (244 VGPRs;
+// the 4-wave 8 x 8-fragment form spills at 256 VGPR + 256 AGPR)
 
 int gemm_f8_config(int cfg, int* bm, int* bn, int* threads) {
   switch (cfg) {
