@@ -262,6 +262,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   X(24, 3, 3, 2, 4, 6, 1)   \
   X(25, 4, 2, 2, 4, 6, 1)   \
   X(26, 6, 3, 2, 4, 3, 2)    \
+  X(27, 5, 2, 2, 4, 3, 2)   \
+  X(28, 5, 3, 2, 4, 3, 2)   \
+  X(29, 5, 4, 2, 4, 2, 2)   \
+  X(30, 5, 2, 2, 4, 4, 1)   \
   X(45, 5, 2, 2, 4, 3, 1)   \
   X(46, 5, 3, 2, 4, 3, 1)   \
   X(47, 5, 4, 2, 4, 3, 1)

@@ -33,7 +33,9 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            32: (4, 2, 2, 4), 33: (4, 4, 2, 2), 34: (3, 3, 2, 4), 35: (4, 4, 2, 2),
            36: (2, 4, 2, 2), 37: (4, 2, 2, 2), 38: (6, 3, 2, 4), 39: (3, 6, 2, 4),
            40: (3, 3, 2, 4), 41: (4, 2, 2, 4), 42: (6, 3, 2, 4),
-           # 160-row LDS-DMA tiles (gemm_pipe.hip ids 45-47): whole waves at the ViT token counts
+           # 160-row LDS-DMA tiles (gemm_pipe.hip ids 45-47): whole waves at the ViT token counts;
+           # 43-45: the same with 64-deep stages (half the barriers over ViT's K = 3072), 46: 4-stage ring
+           43: (5, 2, 2, 4), 44: (5, 3, 2, 4), 45: (5, 4, 2, 4), 46: (5, 2, 2, 4),
            61: (5, 2, 2, 4), 62: (5, 3, 2, 4), 63: (5, 4, 2, 4),
            # warp-specialized fused separable conv (sepconv_ws.hip, KDL_SEPW_CONFIGS): (FM, FN, 1, 4);
            # 127 = s_memtime stamping build of 121 (tools/stamps.py, never a candidate)
