@@ -693,7 +693,12 @@ class Servable:
         # serving_default is warmed eagerly (readiness = its graphs are captured), plus any
         # --warm_signatures (TF-Serving's warmup analogue: engines built before traffic arrives)
         self.runner("serving_default")
-        for name in cfg.warm_signatures:
+        warm = list(cfg.warm_signatures)
+        # f32 requests of exact 8-bit pixels are served by the uint8 signature (grpc_server.py):
+        # build it before traffic too, or the first such request waits for its graph captures
+        if getattr(cfg, "f32_exact_u8", False) and NATIVE_SIGNATURE not in warm:
+            warm.append(NATIVE_SIGNATURE)
+        for name in warm:
             if name in self.signatures:
                 self.runner(name)
 
