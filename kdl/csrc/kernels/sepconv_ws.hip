@@ -103,9 +103,8 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   // same weight fragments at the same time
   int krot = 0;
   if constexpr (KROT) {
-    // a.krot: multiplier (probes); a.wimg (unused by ws) < 0: the N tiles of an M tile also
-    // start half a K loop apart (KDL_WS_NROT probe)
-    krot = (mi * (a.krot > 0 ? a.krot : 7) + (a.wimg < 0 ? ni * (KT / 2) : 0)) % KT;
+    // a.krot > 0: the multiplier (tools probes); 0: 7
+    krot = (mi * (a.krot > 0 ? a.krot : 7)) % KT;
   }
   auto kc = [&](int t) {
     t = min(t, KT - 1) + krot;
@@ -421,12 +420,7 @@ int sepconv_ws_fits(int cfg, int W) {
 }
 
 hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
-  // KDL_WS_KMUL: K-rotation multiplier of the rotated ids (default 7; A/B probes only)
-  static const int env_kmul = [] { const char* e = getenv("KDL_WS_KMUL"); return e ? atoi(e) : 0; }();
-  ConvGemmArgs a = args;
-  if (env_kmul > 0) a.krot = env_kmul;
-  static const int env_nrot = [] { const char* e = getenv("KDL_WS_NROT"); return e ? atoi(e) : 0; }();
-  if (env_nrot > 0) a.wimg = -1;
+  const ConvGemmArgs& a = args;
   int bm, bn, th;
   if (sepconv_ws_config(cfg, &bm, &bn, &th) != 0 || !sepconv_ws_fits(cfg, a.W) || a.K % 32 != 0 ||
       a.K > 8192 || (a.NF * 16) % bn != 0 || a.OH != a.H || a.OW != a.W || a.M <= 0 || a.dwk == nullptr)
