@@ -139,7 +139,7 @@ def main(argv=None) -> int:
     ap.add_argument("--stages", default=None, metavar="STEP",
                     help="stage-pipeline the forward (kdl/engine/stages.py): cut after this step; stage 1 "
                          "of batch i+1 overlaps stage 2 of batch i. Default: the model's cut (Xception: "
-                         "block8_sepconv1 since the fused block2 of round 4; stages measured +10 %% over 2 lanes); 'none' = lanes")
+                         "block8_sepconv3 since the fused entry blocks of round 4; stages measured +10 %% over 2 lanes); 'none' = lanes")
     ap.add_argument("--cu-share", default=None, help="stage CU shares, e.g. 0.6,0.4 (CU-masked stage streams)")
     ap.add_argument("--lanes-free", action="store_true",
                     help="free-running lane streams (LaneGroup.launch_async) instead of forking/joining "

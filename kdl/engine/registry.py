@@ -32,7 +32,7 @@ def _xception():
                      lambda p, max_batch, device, **kw: XceptionEngine(p, max_batch=max_batch, device=device,
                                                                        in_kind="u8", **kw),
                      lambda p, x: X.xception_forward(p, x.float() / 127.5 - 1.0),
-                     stage_cut="block8_sepconv1")
+                     stage_cut="block8_sepconv3")
 
 
 def _resnet50(dtype: str = "fp16"):

@@ -7,8 +7,8 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
     conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
     conv_gemm MODE_PW    residual 1x1/2 convs + BN
     pool_add             TF-'same' 3x3/2 max-pool + residual add
-    entry_block          block2 (both separable convs, the pool and the residual conv) as ONE
-                         persistent launch (kdl/ops/entry_block.py; default, KDL_ENTRY_BLOCK)
+    entry_block          blocks 2 and 3 (both separable convs, the pool and the residual conv)
+                         as ONE persistent launch each (kdl/ops/entry_block.py; KDL_ENTRY_BLOCK)
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
 
 = 41 launches per forward (vs ~168 unfused TF ops), captured into
@@ -43,9 +43,10 @@ class XceptionEngine(EngineBase):
         self.head = head
         # fused entry blocks (entry_block.hip): block numbers lowered to one launch each.
         # KDL_ENTRY_BLOCK: a list "2,3" / "2:4,3" (block[:kernel config]), "1" = blocks 2 and 3,
-        # "0" = none. Default "2:2": block2 with the MFMA depthwise, +2.8 % img/s over the unfused
-        # lowering; adding block3 measured +1.9 % only (profiles/entry_block_ab_r4.txt)
-        eb = os.environ.get("KDL_ENTRY_BLOCK", "2:2")
+        # "0" = none. Default "2:2,3": block2 with the MFMA depthwise (+2.8 % img/s over the unfused
+        # lowering) and block3, whose lighter stage 1 moves the stage cut to block8_sepconv3: +2.0 %
+        # over block2 alone in 4 interleaved pairs (profiles/entry_block_ab_r4.txt)
+        eb = os.environ.get("KDL_ENTRY_BLOCK", "2:2,3")
         spec = "2,3" if eb == "1" else ("" if eb == "0" else eb)
         self.fused_blocks = {}
         for v in filter(None, (x.strip() for x in spec.split(","))):

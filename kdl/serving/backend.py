@@ -361,7 +361,7 @@ class GPUExecutor(_Executor):
             self.lanes.launch(bs[-1], capture=cap)
         # stage pipelining of full top-bucket batches (kdl/engine/stages.py): stage 1 of
         # batch n+1 overlaps stage 2 of batch n. Default: the family's cut (Xception:
-        # after block8_sepconv1) unless lanes were asked for; KDL_STAGES=none disables.
+        # after block8_sepconv3) unless lanes were asked for; KDL_STAGES=none disables.
         self.pipe = None
         cut = self.engine_kwargs.get("stages") or os.environ.get("KDL_STAGES", "")
         if not cut:

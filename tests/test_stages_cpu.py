@@ -117,8 +117,9 @@ def test_xception_default_cut_boundaries():
     from kdl.engine import registry
     cut = registry.get("xception").stage_cut
     sp = _analyse(_xception_steps(), cut, scratch=["__dwtmp"])
-    # the cut is inside middle block 8: its input (block7 output) is the block's residual
-    assert sp.boundary == ["block7_sepconv3_out", "block8_sepconv1_out"]
+    # the cut is after middle block 8 (its sepconv3 adds the residual in its epilogue): one
+    # boundary buffer, the block output
+    assert sp.boundary == ["block8_sepconv3_out"]
     assert sp.wait_for == [1, 1]
 
 
@@ -159,7 +160,7 @@ def test_xception_fused_entry_block_lowering():
     assert len(e.steps) == len(base.steps) - 3
     assert e.shapes["block2_out"] == base.shapes["block2_out"]
     sp = _analyse(e.steps, registry.get("xception").stage_cut, scratch=["__dwtmp"])
-    assert sp.boundary == ["block7_sepconv3_out", "block8_sepconv1_out"]
+    assert sp.boundary == ["block8_sepconv3_out"]
 
 
 def test_entry_block_plan_covers_every_row_once():
