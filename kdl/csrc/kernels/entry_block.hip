@@ -38,7 +38,7 @@ namespace kdl {
 
 __device__ __attribute__((aligned(16))) uint8_t eb_zeros[256];
 
-constexpr int EB_MAX_STEPS = 160;                  // steps per workgroup (host plan checks it)
+constexpr int EB_MAX_STEPS = 128;                  // steps per workgroup (host plan checks it)
 
 template <int C0, int C1, int PC, int NFW, bool DWM = false>
 struct EbGeom {
@@ -67,8 +67,8 @@ struct EbGeom {
   static constexpr int OFF_P = OFF_A + ABYTES;      // per-wave pool rows [NW][PCOLS][16*NFW] bf16
   static constexpr int OFF_DW = OFF_P + NW * PCOLS * 16 * NFW * 2;
   static constexpr int OFF_B = OFF_DW + (KT0 + KT1) * DWQ;   // biases [3][C1] fp32
-  static constexpr int OFF_S = OFF_B + 3 * C1 * 4;  // this workgroup's step table (int4 x MAX_STEPS)
-  static constexpr int BYTES = OFF_S + 16 * EB_MAX_STEPS;
+  static constexpr int OFF_S = OFF_B + 3 * C1 * 4;  // this workgroup's step table, one packed word per step
+  static constexpr int BYTES = OFF_S + 4 * EB_MAX_STEPS;
   static_assert(XROW % 1024 == 0, "whole DMA instructions per x row");
   static_assert(C0 % 32 == 0 && C1 % (16 * NFW) == 0 && NW <= 16, "channel tiling");
   static_assert(BYTES <= 160 * 1024, "LDS");
@@ -175,10 +175,15 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
   uint16_t* const pool = (uint16_t*)(smem + G::OFF_P) + w * (PCOLS * PCH);
   uint32_t* const dwl = (uint32_t*)(smem + G::OFF_DW);
   float* const bl = (float*)(smem + G::OFF_B);
-  int4* const stl = (int4*)(smem + G::OFF_S);
+  uint32_t* const stl = (uint32_t*)(smem + G::OFF_S);
   // the step table goes to LDS once: decoding a step from global memory put an L2 round trip
-  // on every step's critical path twice (measured ~3k cycles per step, tools/ebbench.py --stamps)
-  for (int i = tid; i < s1 - s0; i += 64 * NW) stl[i] = a.steps[s0 + i];
+  // on every step's critical path twice (measured ~3k cycles per step, tools/ebbench.py --stamps).
+  // One word per step {image 8 | strip 6 | pooled row + 2 9 | mode 2 bits}: a 2-workgroup-per-CU
+  // config then fits its 80 KiB (int4 entries took 2 KiB of it)
+  for (int i = tid; i < s1 - s0; i += 64 * NW) {
+    const int4 e = a.steps[s0 + i];
+    stl[i] = (uint32_t)e.x | ((uint32_t)e.y << 8) | ((uint32_t)(e.z + 2) << 14) | ((uint32_t)e.w << 23);
+  }
 
   // ---- depthwise weight entries -> LDS. VALU variant: [k-step][lane group q][tap pair j][channel e]
   // bf16x2; MFMA variant (DWM): pack_dw_entries' [k-step][g][n][parity][8] bf16, 1 KiB per k-step
@@ -237,8 +242,8 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     }
   };
   auto decode = [&](int q, int& b, int& s, int& k, int& mode) {
-    const int4 e = stl[q - s0];
-    b = e.x; s = e.y; k = e.z; mode = e.w;
+    const uint32_t e = stl[q - s0];
+    b = e & 255; s = (e >> 8) & 63; k = (int)((e >> 14) & 511) - 2; mode = (e >> 23) & 3;
   };
   // pooled row k pools y2 rows R..R+2, R = 2k - PT; a step computes y1 rows R+2, R+3 from x rows
   // R+1..R+4: the rows its predecessor did not load (a run's first step loads all four)
@@ -509,7 +514,8 @@ static int eb_pad(int cfg) {
 hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
   int c0, c1, pc, lds, occ;
   if (entry_block_config(cfg, &c0, &c1, &pc, &lds, &occ) != 0 || a.ldx != c0 || a.ldy != c1 || a.grid < 1 ||
-      a.OH != (a.H - 1) / 2 + 1 || a.OW != (a.W - 1) / 2 + 1 || a.H != a.W || !a.steps || !a.step_off)
+      a.OH != (a.H - 1) / 2 + 1 || a.OW != (a.W - 1) / 2 + 1 || a.H != a.W || !a.steps || !a.step_off ||
+      a.B > 256)                                     // the packed LDS step word holds an 8-bit image index
     return hipErrorInvalidValue;
   if (eb_pad(cfg) != (a.H % 2)) return hipErrorInvalidValue;   // TF 'same': leading pad 1 iff odd size
   switch (cfg) {

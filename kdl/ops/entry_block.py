@@ -21,7 +21,7 @@ from .conv import MODE_DW, MODE_PW, ConvGemmLayer
 
 # mode of a step (EntryBlockArgs.steps[i].w)
 WARM_Y1, WARM_Y2, OUT = 0, 1, 2
-MAX_STEPS = 160          # entry_block.hip EB_MAX_STEPS: a workgroup's step table lives in LDS
+MAX_STEPS = 128          # entry_block.hip EB_MAX_STEPS: a workgroup's step table lives in LDS
 
 
 def entry_block_config(cfg: int) -> tuple[int, int, int, int, int]:
