@@ -103,7 +103,11 @@ class XceptionEngine(EngineBase):
                 if bi + 1 in self.fused_blocks:
                     from ..ops.entry_block import EntryBlock
                     s1, s2 = (self._sep(p, op, dev) for op in blk.main)
-                    fb = EntryBlock(f"block{bi + 1}", s1, s2, lay, cfg=self.fused_blocks[bi + 1], device=dev)
+                    # KDL_ENTRY_GRID: workgroups per fused block launch (default one per CU per
+                    # resident workgroup); fewer leave CUs to the other pipeline stage
+                    g = os.environ.get("KDL_ENTRY_GRID")
+                    fb = EntryBlock(f"block{bi + 1}", s1, s2, lay, cfg=self.fused_blocks[bi + 1], device=dev,
+                                    grid=int(g) if g else None)
                     self.steps.append(Step("block", f"block{bi + 1}", src=cur, dst=out, geom=(H, H, oh, oh),
                                            extra=dict(eb=fb)))
                     self.shapes[out] = (oh, oh, s2.ldy)
