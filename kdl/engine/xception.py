@@ -11,7 +11,8 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
                          as ONE persistent launch each (kdl/ops/entry_block.py; KDL_ENTRY_BLOCK)
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
 
-= 41 launches per forward (vs ~168 unfused TF ops), captured into
+= 44 launches per forward with the tuned table (vs ~168 unfused TF ops; split
+separable convs count twice: depthwise + GEMM), captured into
 one hipGraph per batch bucket. All buffers are allocated once for the largest
 bucket (static memory plan); smaller buckets use prefixes of the same buffers.
 The reference equivalent is TF-Serving's SavedModel session run
