@@ -47,13 +47,14 @@ def test_gemm_f8_fp8_output():
     sa = x.abs().max().item() / 448
     x8 = to_e4m3(x / sa).to(DEV)
     lay = F8Linear("t", torch.randn(N, K, generator=gen) / K ** 0.5, torch.zeros(N), sa, device=DEV)
-    y8 = torch.zeros(M, N, dtype=torch.uint8, device=DEV)
     so = 0.02
-    lay.emit(None, x8=x8.data_ptr(), M=M, y8=y8.data_ptr(), out_scale=so)
-    torch.cuda.synchronize()
     ref = (from_e4m3(x8.cpu()) * sa) @ lay.w_ref.t()
-    got = from_e4m3(y8.cpu()) * so
-    assert ((got - ref).abs().max() / ref.abs().max()).item() < 0.08     # e4m3 output rounding (3 mantissa bits)
+    for cfg in lay.candidates:                 # incl. the persistent direct-epilogue configs (32-37)
+        y8 = torch.zeros(M, N, dtype=torch.uint8, device=DEV)
+        lay.emit(None, cfg=cfg, x8=x8.data_ptr(), M=M, y8=y8.data_ptr(), out_scale=so)
+        torch.cuda.synchronize()
+        got = from_e4m3(y8.cpu()) * so
+        assert ((got - ref).abs().max() / ref.abs().max()).item() < 0.08, cfg   # e4m3 output rounding
 
 
 def test_vit_fp8_engine_matches_oracle():
