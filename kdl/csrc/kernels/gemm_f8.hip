@@ -161,134 +161,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
   }
 }
 
-// Persistent variant: the ViT linears have K = 768 (QKV, out_proj, mlp.0): six 128-deep k-steps per
-// tile, so a one-tile-per-workgroup launch spends much of each tile filling its ring and draining
-// through the LDS C tile. Here each workgroup walks tiles wg, wg + G, ... as ONE stream of
-// (tile, k-step) stages: the ring keeps loading the next tile's first stages while the current
-// tile finishes, and the epilogue writes straight from the accumulators (each lane: 4 consecutive
-// columns of one row) with no LDS round trip and no barrier.
-template <int FM, int FN, int WGM, int WGN, int STAGES>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_persist_kernel(GemmF8Args a, int G) {
-  constexpr int NW = WGM * WGN;
-  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
-  constexpr int AF = BM / 16, BF = BN / 16;
-  constexpr int HF = 2 * (AF + BF);
-  constexpr int L = (HF + NW - 1) / NW;
-  constexpr int STAGE = HF * 1024;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[STAGES * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WGN, wn = wave % WGN;
-  const int nN = (a.NF * 16) / BN;
-  const int nM = (a.M + BM - 1) / BM;
-  const int tiles = nM * nN;
-  const int wg = xcd_remap(blockIdx.x, G);
-  const int mine = wg < tiles ? (tiles - 1 - wg) / G + 1 : 0;   // tiles wg, wg + G, ...
-  const int KT = a.K >> 7;
-  const int U = mine * KT;                                      // (tile, k-step) stages of this workgroup
-  if (U == 0) return;
-
-  auto issue = [&](int u, int buf) {
-    const int tile = wg + (u / KT) * G;
-    const int mi = tile / nN, ni = tile - mi * nN;
-    int t = u % KT + (a.krot ? (mi * 7) % KT : 0);
-    t = t >= KT ? t - KT : t;
-    uint8_t* base = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < L; ++i) {
-      const int hf = min(wave + i * NW, HF - 1);
-      const int f = hf >> 1, h = hf & 1;
-      if (f < AF) {
-        int m = mi * BM + f * 16 + (lane & 15);
-        m = m < a.M ? m : a.M - 1;
-        glds16(a.x + (long)m * a.ldx + 32 * (lane >> 4) + 16 * h + (long)t * 128, base + hf * 1024);
-      } else {
-        const int nf = ni * BN / 16 + (f - AF);
-        glds16(a.wp + ((long)nf * KT * 2 + h) * 1024 + lane * 16 + (long)t * 2048, base + hf * 1024);
-      }
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int p = 0; p < STAGES - 1; ++p)
-    if (p < U) issue(p, p);
-
-  const int quad = lane >> 4, col = lane & 15;
-  for (int u = 0; u < U; ++u) {
-    const int after = min(U - 1, u + STAGES - 2) - u;
-    if (after >= 2) f8_wait_barrier<2 * L>();
-    else if (after == 1) f8_wait_barrier<L>();
-    else f8_wait_barrier<0>();
-    if (u + STAGES - 1 < U) issue(u + STAGES - 1, (u + STAGES - 1) % STAGES);
-    const uint8_t* st = smem + (u % STAGES) * STAGE + lane * 16;
-    v8i af[FM], bf[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const u32x4 lo = *(const u32x4*)(st + ((wm * FM + i) * 2) * 1024);
-      const u32x4 hi = *(const u32x4*)(st + ((wm * FM + i) * 2 + 1) * 1024);
-      af[i] = (v8i){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const u32x4 lo = *(const u32x4*)(st + ((AF + wn * FN + j) * 2) * 1024);
-      const u32x4 hi = *(const u32x4*)(st + ((AF + wn * FN + j) * 2 + 1) * 1024);
-      bf[j] = (v8i){(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[i][j], 0, 0, 0, 127, 0, 127);
-    __builtin_amdgcn_s_setprio(0);
-    if (u % KT != KT - 1) continue;
-    // ---- tile done: direct epilogue (scale, bias, activation, residual, bf16 / e4m3 store)
-    const int tile = wg + (u / KT) * G;
-    const int mi = tile / nN, ni = tile - mi * nN;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = ni * BN + (wn * FN + j) * 16 + 4 * quad;
-      const float4 bv = *(const float4*)(a.bias + n);
-      const float4 sv = *(const float4*)(a.colscale + n);
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = mi * BM + (wm * FM + i) * 16 + col;
-        float v0 = acc[i][j][0] * sv.x + bv.x, v1 = acc[i][j][1] * sv.y + bv.y;
-        float v2 = acc[i][j][2] * sv.z + bv.z, v3 = acc[i][j][3] * sv.w + bv.w;
-        acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if (m >= a.M || n >= a.nstore) continue;
-        if (a.relu_out == 1) {
-          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-        }
-        u32x2 v = {pack_bf16(v0, v1), pack_bf16(v2, v3)};
-        if (a.relu_out >= 3) {
-          const u32x4 t4 = act_transcendental(a.relu_out, (u32x4){v[0], v[1], 0u, 0u});
-          v = (u32x2){t4[0], t4[1]};
-        }
-        if (a.res) {
-          const u32x2 rv = *(const u32x2*)(a.res + (long)m * a.ldr + n);
-#pragma unroll
-          for (int d = 0; d < 2; ++d) v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
-        }
-        if (a.y8) {
-          const float q = a.out_inv_scale;
-          *(uint32_t*)(a.y8 + (long)m * a.ldy + n) =
-              pack_fp8x4(bf_lo(v[0]) * q, bf_hi(v[0]) * q, bf_lo(v[1]) * q, bf_hi(v[1]) * q);
-        } else {
-          *(u32x2*)(a.y + (long)m * a.ldy + n) = v;
-        }
-      }
-    }
-  }
-}
-
 // (FM, FN, WGM, WGN, STAGES)
 #define KDL_F8_CONFIGS(X) \
   X(0, 4, 4, 2, 2, 2)     \
@@ -311,24 +183,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_persist_kernel(GemmF8A
   X(17, 6, 4, 2, 4, 2)
 // 8-10: 160-row tiles, whole waves of 256 CUs at the ViT-B/16 token count (gemm_pipe.hip 45-47);
 // 11-15: 3-4 stage rings of the large tiles (2 stages leave one k-step of load latency exposed)
-// 32-37 (KDL_F8P_CONFIGS): gemm_f8_persist_kernel, (FM, FN, WGM, WGN, STAGES, workgroups per CU)
-#define KDL_F8P_CONFIGS(X)    \
-  X(32, 5, 2, 2, 4, 3, 1)     \
-  X(33, 4, 2, 2, 4, 3, 1)     \
-  X(34, 5, 4, 2, 4, 2, 1)     \
-  X(35, 4, 4, 2, 4, 3, 1)     \
-  X(36, 4, 2, 2, 4, 2, 2)     \
-  X(37, 5, 2, 2, 4, 4, 1)
 // 16-17: 256 x 256 / 192 x 256 tiles: at 128-deep fp8 k-steps a 160 x 128 tile needs ~57 B/clk per CU
 // to keep the MFMAs busy, more than an L2-fed CU takes in (~28-30); 256 x 256 needs ~32 (244 VGPRs;
 // the 4-wave 8 x 8-fragment form spills at 256 VGPR + 256 AGPR)
 
 int gemm_f8_config(int cfg, int* bm, int* bn, int* threads) {
   switch (cfg) {
-#define KDL_F8PINFO(id, fm, fn, wgm, wgn, st, occ) \
-  case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
-    KDL_F8P_CONFIGS(KDL_F8PINFO)
-#undef KDL_F8PINFO
 #define KDL_F8INFO(id, fm, fn, wgm, wgn, st) \
   case id: *bm = 16 * fm * wgm; *bn = 16 * fn * wgn; *threads = 64 * wgm * wgn; return 0;
     KDL_F8_CONFIGS(KDL_F8INFO)
@@ -346,20 +206,7 @@ hipError_t gemm_f8(int cfg, const GemmF8Args& args, hipStream_t s) {
       a.M <= 0)
     return hipErrorInvalidValue;
   const int grid = ((a.M + bm - 1) / bm) * ((a.NF * 16) / bn);
-  static const int ncu = [] {
-    int d = 0, n = 0;
-    (void)hipGetDevice(&d);
-    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
-  }();
   switch (cfg) {
-#define KDL_F8PCASE(id, fm, fn, wgm, wgn, st, occ)                                                        \
-  case id: {                                                                                             \
-    const int G = grid < occ * ncu ? grid : occ * ncu;                                                   \
-    hipLaunchKernelGGL((gemm_f8_persist_kernel<fm, fn, wgm, wgn, st>), dim3(G), dim3(th), 0, s, a, G);   \
-    break;                                                                                               \
-  }
-    KDL_F8P_CONFIGS(KDL_F8PCASE)
-#undef KDL_F8PCASE
 #define KDL_F8CASE(id, fm, fn, wgm, wgn, st) \
   case id: hipLaunchKernelGGL((gemm_f8_kernel<fm, fn, wgm, wgn, st>), dim3(grid), dim3(th), 0, s, a); break;
     KDL_F8_CONFIGS(KDL_F8CASE)

@@ -18,10 +18,7 @@ F8_CONFIGS = {0: (4, 4, 2, 2, 2), 1: (4, 4, 2, 2, 3), 2: (2, 4, 2, 2, 3), 3: (4,
               4: (3, 3, 2, 4, 2), 5: (6, 3, 2, 4, 2), 6: (3, 6, 2, 4, 2), 7: (4, 4, 2, 4, 2),
               8: (5, 2, 2, 4, 2), 9: (5, 3, 2, 4, 2), 10: (5, 4, 2, 4, 2),
               11: (4, 4, 2, 4, 3), 12: (5, 2, 2, 4, 3), 13: (4, 2, 2, 4, 3), 14: (5, 2, 2, 4, 4),
-              15: (4, 2, 2, 4, 4), 16: (8, 4, 2, 4, 2), 17: (6, 4, 2, 4, 2),
-              # 32-37: persistent (tile, k-step) stream per workgroup, direct epilogue (gemm_f8.hip)
-              32: (5, 2, 2, 4, 3), 33: (4, 2, 2, 4, 3), 34: (5, 4, 2, 4, 2), 35: (4, 4, 2, 4, 3),
-              36: (4, 2, 2, 4, 2), 37: (5, 2, 2, 4, 4)}
+              15: (4, 2, 2, 4, 4), 16: (8, 4, 2, 4, 2), 17: (6, 4, 2, 4, 2)}
 
 
 def f8_tile(cfg: int) -> tuple[int, int]:
