@@ -188,8 +188,11 @@ class XceptionEngine(EngineBase):
         w[:, :op.cin] = p[f"{op.name}/pointwise_kernel"].double()[0, 0].t() * s[:, None]
         dww = torch.zeros(9, cin_pad, dtype=torch.float32)
         dww[:, :op.cin] = p[f"{op.name}/depthwise_kernel"].float()[:, :, :, 0].reshape(9, op.cin)
+        # block14 (10x10 maps: M = 3,200 rows at batch 32, 160-200 output tiles): split-K candidates
+        # for its split lowering's GEMM
         return ConvGemmLayer(op.name, MODE_DW, w, t, cin_pad=cin_pad, n=op.cout, dww=dww,
-                             relu_in=op.relu_in, relu_out=op.relu_out, device=dev)
+                             relu_in=op.relu_in, relu_out=op.relu_out, device=dev,
+                             ksplit=(2, 3, 4) if op.cout >= 1536 else ())
 
     def _alloc(self) -> None:
         B, S, dev = self.max_batch, self.size, self.device

@@ -227,7 +227,7 @@ class ConvGemmLayer:
         # keep an fp32 copy of the exact (bf16-rounded) weights for reference checks
         self.w_ref = w_nk.to(dtype).float()
         self.ksplit = tuple(ksplit)
-        assert not self.ksplit or mode in (MODE_PW, MODE_CONV), (name, "split-K: LDS-DMA GEMM lowerings only")
+        assert not self.ksplit or mode in (MODE_PW, MODE_CONV, MODE_DW), (name, "split-K: LDS-DMA GEMM lowerings only")
         self._splitk_bufs: tuple | None = None     # (fp32 partials, per-tile counters), grown on demand
         self.w_plain = None
         if blaslt:
@@ -249,9 +249,10 @@ class ConvGemmLayer:
         if self.mode != MODE_DW:
             blt = [(False, BLT_BASE + i) for i in range(BLT_ALGOS)] if self.w_plain is not None else []
             return [(False, c) for c in self.candidates if c < SEP_BASE] + blt + skv
+        # separable conv: fused configs, or the split lowering (depthwise, then a plain GEMM -- split-K too)
         return ([(False, c) for c in self.candidates
                  if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W, self.K, self.n)]
-                + [(True, c) for c in self.candidates if c < SEP_BASE])
+                + [(True, c) for c in self.candidates if c < SEP_BASE] + [(True, c) for _, c in skv])
 
     def dw_args(self, x: int, tmp: int, g: Geometry, ldx: int | None = None) -> dict:
         assert (ldx or self.cin_pad) == self.cin_pad
@@ -275,7 +276,13 @@ class ConvGemmLayer:
         if self.mode == MODE_DW and split:
             assert tmp is not None, "split separable conv needs a scratch buffer"
             da = self.dw_args(x, tmp, g, ldx)
-            ga = self.args(tmp, y, g, res, ldx=self.cin_pad, ldr=ldr, cfg=cfg, opad=opad)
+            if is_splitk(cfg):
+                sk, cfg = splitk_parts(cfg)
+                ga = self.args(tmp, y, g, res, ldx=self.cin_pad, ldr=ldr, cfg=cfg, opad=opad)
+                ws, cnt = self._splitk_workspace(sk, cfg, g.M)
+                ga.update(ksplit=sk, ws=_lib.ptr(ws), cnt=_lib.ptr(cnt))
+            else:
+                ga = self.args(tmp, y, g, res, ldx=self.cin_pad, ldr=ldr, cfg=cfg, opad=opad)
             if prog is None:
                 s = _lib.stream_ptr()
                 C.dw3x3(da, s)
