@@ -71,3 +71,29 @@ def test_splitk_residual_epilogue_in_captured_graph():
             first = y.clone()
         assert torch.equal(y, first)
     assert int(lay._splitk_bufs[1].abs().sum()) == 0      # every tile's counter reset by its last split
+
+
+def test_splitk_in_the_split_separable_lowering():
+    """Xception block14 shapes (10x10 maps): depthwise into scratch, then the split-K GEMM with the
+    residual-free BN epilogue; every split-K id the layer offers, twice (counters reset)."""
+    from kdl.ops.reference import conv_gemm_ref
+    from kdl.ops.conv import MODE_DW, is_splitk
+    gen = torch.Generator().manual_seed(14)
+    B, H, cin, n = 4, 10, 1024, 1536
+    w = torch.randn(n, cin, generator=gen, dtype=torch.float64) / cin ** 0.5
+    dww = torch.randn(9, cin, generator=gen) / 3
+    b = torch.randn(n, generator=gen) * 0.1
+    lay = ConvGemmLayer("b14", MODE_DW, w, b, cin_pad=cin, n=n, dww=dww, relu_in=True, relu_out=1,
+                        device=DEV, ksplit=(2, 3, 4))
+    g = Geometry(B, H, H, H, H)
+    x = torch.randn(B, H, H, cin, generator=gen).to(torch.bfloat16).to(DEV).contiguous()
+    ref = conv_gemm_ref(lay, x, g)
+    tmp = torch.empty(B * H * H * cin, dtype=torch.bfloat16, device=DEV)
+    ids = [c for split, c in lay.variants(H) if split and is_splitk(c)]
+    assert ids, "no split-K variant offered"
+    for cfg in ids:
+        for _ in range(2):
+            y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+            lay.emit(None, x.data_ptr(), y.data_ptr(), g, tmp=tmp.data_ptr(), split=True, cfg=cfg)
+            torch.cuda.synchronize()
+            assert _rel(y.view(g.M, lay.ldy)[:, :n], ref.reshape(g.M, -1)[:, :n]) < 2e-2, cfg
