@@ -346,6 +346,17 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     if (q + 1 < s1) dma_for(q + 1);
 
     // ---- P2: GEMM1 (+ bias, ReLU) -> y1 ring rows R+2, R+3; residual GEMM
+    // HOIST (1-slice configs, registers to spare): every A fragment is read before the first y1
+    // store -- the compiler cannot move a read above a store it cannot prove disjoint, which
+    // chained each fragment's LDS latency behind the previous fragment's store
+    constexpr bool HOIST = NFW == 1 && OCC == 1;
+    s16x8 a1h[HOIST ? Y1F : 1][KT0];
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int f = 0; f < Y1F; ++f)
+#pragma unroll
+        for (int t = 0; t < KT0; ++t) a1h[f][t] = *(const s16x8*)(Ab + (t * Y1F + f) * 1024 + lane * 16);
+    }
 #pragma unroll
     for (int f = 0; f < Y1F; ++f) {
       const s16x8* af = (const s16x8*)(Ab + f * 1024 + lane * 16);
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
       for (int n = 0; n < NFW; ++n) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < KT0; ++t) acc = mfma16(w1[n][t], af[t * Y1F * 64], acc);
+        for (int t = 0; t < KT0; ++t) acc = mfma16(w1[n][t], HOIST ? a1h[HOIST ? f : 0][t] : af[t * Y1F * 64], acc);
         if (pi < 2 * Y1C) {
           const int c = PCH * w + 16 * n + 4 * q16;
           const float4 bv = bias(0, n);
@@ -407,6 +418,13 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     // ---- P4: GEMM2 + bias -> bf16 values; vertical max with the carried row
     const bool r0ok = (unsigned)R < (unsigned)H && mode == 2, r1ok = (unsigned)(R + 1) < (unsigned)H;
     const bool r2ok = (unsigned)(R + 2) < (unsigned)H;
+    s16x8 a2h[HOIST ? Y2F : 1][KT1];                 // HOIST: every fragment read before the pool stores
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int f = 0; f < Y2F; ++f)
+#pragma unroll
+        for (int t = 0; t < KT1; ++t) a2h[f][t] = *(const s16x8*)(Ab + (t * Y2F + f) * 1024 + lane * 16);
+    }
 #pragma unroll
     for (int fc = 0; fc < Y2FR; ++fc) {
       const s16x8* a0 = (const s16x8*)(Ab + fc * 1024 + lane * 16);
@@ -418,8 +436,8 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < KT1; ++t) {
-          acc0 = mfma16(w2[n][t], a0[t * Y2F * 64], acc0);
-          acc1 = mfma16(w2[n][t], a1[t * Y2F * 64], acc1);
+          acc0 = mfma16(w2[n][t], HOIST ? a2h[HOIST ? fc : 0][t] : a0[t * Y2F * 64], acc0);
+          acc1 = mfma16(w2[n][t], HOIST ? a2h[HOIST ? Y2FR + fc : 0][t] : a1[t * Y2F * 64], acc1);
         }
         float vm[4];
         const float4 b4 = bias(1, n);
