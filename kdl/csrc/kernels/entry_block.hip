@@ -119,8 +119,8 @@ __device__ __forceinline__ s16x8 eb_dw8(Tap tap, const uint32_t* wq) {
 // (pack_dw_entries) of channel 16g + p16, tap parity kb >> 1. The C fragment [16 ch][16 px] is
 // written transposed into the unit's lane-linear A fragment at dst.
 template <bool RELU, class Tap, class Ent>
-__device__ __forceinline__ void eb_dw_mfma(Tap tap, Ent ent, uint8_t* dst, int lane, const uint32_t (&sel)[2][4]) {
-  const int p16 = lane & 15, kb = lane >> 4, par = kb >> 1;
+__device__ __forceinline__ void eb_dw_mfma_vals(Tap tap, Ent ent, int lane, const uint32_t (&sel)[2][4], u32x2 (&out)[2]) {
+  const int kb = lane >> 4, par = kb >> 1;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const u32x4 we = ent(g);
@@ -139,9 +139,17 @@ __device__ __forceinline__ void eb_dw_mfma(Tap tap, Ent ent, uint8_t* dst, int l
       for (int d = 0; d < 4; ++d) wf[d] = __builtin_amdgcn_perm(wd, wd, sel[j & 1][d]);
       acc = mfma16(__builtin_bit_cast(s16x8, wf), __builtin_bit_cast(s16x8, v), acc);
     }
-    *(u32x2*)(dst + (p16 + 16 * (2 * g + par)) * 16 + 8 * (kb & 1)) =
-        (u32x2){pack_bf16(acc[0], acc[1]), pack_bf16(acc[2], acc[3])};
+    out[g] = (u32x2){pack_bf16(acc[0], acc[1]), pack_bf16(acc[2], acc[3])};
   }
+}
+
+// the C fragment [16 ch][16 px] of both channel groups, written transposed into the unit's
+// lane-linear A fragment at dst. Kept apart from the MFMAs so a phase can compute all of its
+// units before its first store (a later unit's tap reads would otherwise wait behind it)
+__device__ __forceinline__ void eb_dw_store(uint8_t* dst, int lane, const u32x2 (&out)[2]) {
+  const int p16 = lane & 15, kb = lane >> 4, par = kb >> 1;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) *(u32x2*)(dst + (p16 + 16 * (2 * g + par)) * 16 + 8 * (kb & 1)) = out[g];
 }
 
 __device__ __forceinline__ s16x8 eb_frag(const uint16_t* wp, int nf, int kt, int t, int lane) {
@@ -295,6 +303,10 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     // 2k = R+1) or k+1 (PT 0: x row 2k+2 = R+2; x row 2k is no longer in the ring)
     {
       const uint32_t* wq = dwl + (t1 * 4 + q16) * 40;
+      u32x2 dv[U1W][2];                              // DWM: every unit's outputs, stored after the loop
+      uint8_t* ddst[U1W];
+#pragma unroll
+      for (int i = 0; i < U1W; ++i) ddst[i] = nullptr;
 #pragma unroll
       for (int i = 0; i < U1W; ++i) {
         const int u = w + NW * i;
@@ -312,7 +324,8 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             auto ent = [&](int g) {
               return *(const u32x4*)((const uint8_t*)dwl + t1 * G::DWQ + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
             };
-            eb_dw_mfma<RELU1>(tap, ent, Ab + (t1 * Y1F + f) * 1024, lane, sel);
+            eb_dw_mfma_vals<RELU1>(tap, ent, lane, sel, dv[i]);
+            ddst[i] = Ab + (t1 * Y1F + f) * 1024;
           } else {
             const uint8_t* base = xr + (4 * t1 + q16) * PLB + col * 16;
             auto tap = [&](int ti) {
@@ -321,6 +334,11 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             *(s16x8*)(Ab + (t1 * Y1F + f) * 1024 + lane * 16) = eb_dw8<RELU1>(tap, wq);
           }
         }
+      }
+      if constexpr (DWM) {
+#pragma unroll
+        for (int i = 0; i < U1W; ++i)
+          if (ddst[i]) eb_dw_store(ddst[i], lane, dv[i]);
       }
     }
     if (PT == 1 ? mode == 2 : mode >= 1) {           // residual 1x1/2 conv of its pooled row
@@ -386,6 +404,10 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     // ---- P3: depthwise 2 -> A (y2 rows R+1, R+2: fragments [row][col / 16])
     {
       const uint32_t* wq = dwl + ((KT0 + t2) * 4 + q16) * 40;
+      u32x2 dv2[U2W][2];
+      uint8_t* ddst2[U2W];
+#pragma unroll
+      for (int i = 0; i < U2W; ++i) ddst2[i] = nullptr;
 #pragma unroll
       for (int i = 0; i < U2W; ++i) {
         const int u = w + NW * i;
@@ -401,7 +423,8 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             auto ent = [&](int g) {
               return *(const u32x4*)((const uint8_t*)dwl + (KT0 + t2) * G::DWQ + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
             };
-            eb_dw_mfma<false>(tap, ent, Ab + (t2 * Y2F + f) * 1024, lane, sel);
+            eb_dw_mfma_vals<false>(tap, ent, lane, sel, dv2[i]);
+            ddst2[i] = Ab + (t2 * Y2F + f) * 1024;
           } else {
             const uint8_t* base = y1r + (4 * t2 + q16) * PLB + col * 16;
             auto tap = [&](int ti) {
@@ -410,6 +433,11 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             *(s16x8*)(Ab + (t2 * Y2F + f) * 1024 + lane * 16) = eb_dw8<false>(tap, wq);
           }
         }
+      }
+      if constexpr (DWM) {
+#pragma unroll
+        for (int i = 0; i < U2W; ++i)
+          if (ddst2[i]) eb_dw_store(ddst2[i], lane, dv2[i]);
       }
     }
     __syncthreads();                                 // B3: A (y2) complete
