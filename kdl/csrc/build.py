@@ -92,8 +92,12 @@ def build_gpu(force: bool = False, njobs: int = 8, verbose: bool = True) -> Path
         # hipBLASLt (the vendor GEMM node, runtime/blaslt.cpp): SONAME libhipblaslt.so.1, the same
         # as the copy torch loads first (import torch precedes kdl._C), so one instance is shared;
         # the same holds for RCCL (runtime/comm.cpp, SONAME librccl.so.1)
+        # link to a temporary name, then rename: a reader (an import, a tree snapshot) sees the old
+        # or the new library, never a half-written one
+        tmp = out.with_name(out.name + ".tmp")
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-L/opt/rocm/lib",
-              "-lhipblaslt", "-lrccl", "-o", str(out)])
+              "-lhipblaslt", "-lrccl", "-o", str(tmp)])
+        os.replace(tmp, out)
         if verbose:
             print(f"[kdl.build] linked {out.relative_to(ROOT)}", flush=True)
     return out
@@ -114,7 +118,9 @@ def build_rt(force: bool = False, njobs: int = 8, verbose: bool = True) -> Path:
         print(f"[kdl.build] compiling {len(jobs)} runtime source(s)", flush=True)
     _compile_all(jobs, njobs)
     if force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
-        _run([cxx, "-shared", "-fPIC", "-pthread", *map(str, objs), "-o", str(out)])
+        tmp = out.with_name(out.name + ".tmp")
+        _run([cxx, "-shared", "-fPIC", "-pthread", *map(str, objs), "-o", str(tmp)])
+        os.replace(tmp, out)
         if verbose:
             print(f"[kdl.build] linked {out.relative_to(ROOT)}", flush=True)
     return out
