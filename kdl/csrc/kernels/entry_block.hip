@@ -223,7 +223,22 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
   }
   for (int i = tid; i < 3 * C1; i += 64 * NW) bl[i] = (i < C1 ? a.b1 : i < 2 * C1 ? a.b2 : a.br)[i % C1];
   // this lane's 4 accumulator channels of output slice n: bias (LDS) of GEMM g (0 pw1, 1 pw2, 2 residual)
-  auto bias = [&](int g, int n) { return *(const float4*)(bl + g * C1 + PCH * w + 16 * n + 4 * q16); };
+  // 1-slice configs keep this lane's 3 x 4 biases in registers (read once from global): in LDS a
+  // bias read that follows a y1 / pool store cannot be hoisted above it, so every fragment of
+  // P2 / P4 re-read it and waited for it
+  constexpr bool BREG = NFW == 1 && OCC == 1;
+  float4 breg[BREG ? 3 : 1][NFW];
+  if constexpr (BREG) {
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+      for (int n = 0; n < NFW; ++n)
+        breg[g][n] = *(const float4*)((g == 0 ? a.b1 : g == 1 ? a.b2 : a.br) + PCH * w + 16 * n + 4 * q16);
+  }
+  auto bias = [&](int g, int n) {
+    if constexpr (BREG) return breg[g][n];
+    else return *(const float4*)(bl + g * C1 + PCH * w + 16 * n + 4 * q16);
+  };
   const int t1 = w % KT0, t2 = w % KT1;              // every depthwise unit of this wave uses these k-steps
   uint32_t sel[2][4];                                // DWM: v_perm selectors of the block-diagonal operand
   {
@@ -238,35 +253,9 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
         sel[jp][d] = (wv && (e >> 1) == d) ? val : 0x0c0c0c0cu;
       }
   }
-  // ---- x row DMA: row r of image b, strip columns from global col gx0, into ring slot r & 3.
-  // Prepared (step decode from LDS, per-lane addresses) before the barrier that frees the ring
-  // slots and only issued after it, so the issue is a few glds instructions on the critical path
-  constexpr int DMAW = (4 * G::XDMA + NW - 1) / NW;   // DMA instructions per wave, at most
-  const uint8_t* dma_src[DMAW];
-  uint8_t* dma_dst[DMAW];
-  int dma_n = 0;
-  auto dma_prep = [&](int b, int gx0, int r0, int nr) {
-    dma_n = 0;
-#pragma unroll
-    for (int k = 0; k < DMAW; ++k) {
-      const int ii = w + k * NW;
-      if (ii < nr * G::XDMA) {
-        const int r = r0 + ii / G::XDMA, d = ii % G::XDMA;
-        const int slot = d * 64 + lane, plane = slot / PLP, px = slot - plane * PLP;
-        const int gx = gx0 + px;
-        const bool ok = px < XC && (unsigned)r < (unsigned)H && (unsigned)gx < (unsigned)W;
-        dma_src[k] = ok ? (const uint8_t*)(a.x + (((long)b * H + r) * W + gx) * a.ldx + plane * 8) : eb_zeros;
-        dma_dst[k] = xr + (r & 3) * XROW + d * 1024;
-        dma_n = k + 1;
-      }
-    }
-  };
-  auto dma_issue = [&]() {
-#pragma unroll
-    for (int k = 0; k < DMAW; ++k)
-      if (k < dma_n) glds16(dma_src[k], dma_dst[k]);
-  };
-  auto dma_rows = [&](int b, int gx0, int r0, int nr) {   // prepare + issue at once (no live arrays)
+  // ---- x row DMA: row r of image b, strip columns from global col gx0, into ring slot r & 3
+  // (preparing the addresses ahead, before B1, measured slower: the wave runs it in order anyway)
+  auto dma_rows = [&](int b, int gx0, int r0, int nr) {
     for (int ii = w; ii < nr * G::XDMA; ii += NW) {
       const int r = r0 + ii / G::XDMA, d = ii % G::XDMA;
       const int slot = d * 64 + lane, plane = slot / PLP, px = slot - plane * PLP;
@@ -282,14 +271,6 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
   };
   // pooled row k pools y2 rows R..R+2, R = 2k - PT; a step computes y1 rows R+2, R+3 from x rows
   // R+1..R+4: the rows its predecessor did not load (a run's first step loads all four)
-  auto dma_prep_for = [&](int q) {
-    int b, s, k, mode;
-    decode(q, b, s, k, mode);
-    const int R = 2 * k - PT;
-    const int gx0 = 2 * s * PC - PT - 2;
-    if (mode == 0) dma_prep(b, gx0, R + 1, 4);
-    else dma_prep(b, gx0, R + 3, 2);
-  };
   auto dma_for = [&](int q) {
     int b, s, k, mode;
     decode(q, b, s, k, mode);
@@ -332,10 +313,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     for (int n = 0; n < NFW; ++n) acco[n] = accr[n];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();                                 // B0: x rows landed; previous step done
-    // PREP (registers to spare): the next step's DMA addresses are computed here, off the
-    // critical path after B1; otherwise (block3's 2-slice config) both after B1
-    constexpr bool PREP = NFW == 1 && OCC == 1;
-    if (PREP && q + 1 < s1) dma_prep_for(q + 1);
+
     stamp(q, 0);
 
     // ---- P1: depthwise 1 -> A (y1 rows R+2, R+3); residual operands: pooled row k (PT 1: x row
@@ -400,10 +378,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
       for (int n = 0; n < NFW; ++n) *(u32x2*)(st_ptr + 16 * n) = st_val[n];
       st_pend = false;
     }
-    if (q + 1 < s1) {
-      if constexpr (PREP) dma_issue();
-      else dma_for(q + 1);
-    }
+    if (q + 1 < s1) dma_for(q + 1);
 
     // ---- P2: GEMM1 (+ bias, ReLU) -> y1 ring rows R+2, R+3; residual GEMM
     // HOIST (1-slice configs, registers to spare): every A fragment is read before the first y1
