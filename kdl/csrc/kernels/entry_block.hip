@@ -392,6 +392,9 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
 #pragma unroll
         for (int t = 0; t < KT0; ++t) a1h[f][t] = *(const s16x8*)(Ab + (t * Y1F + f) * 1024 + lane * 16);
     }
+    float4 bz0[NFW];                                 // read before the y1 stores (see BREG)
+#pragma unroll
+    for (int n = 0; n < NFW; ++n) bz0[n] = bias(0, n);
 #pragma unroll
     for (int f = 0; f < Y1F; ++f) {
       const s16x8* af = (const s16x8*)(Ab + f * 1024 + lane * 16);
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
         for (int t = 0; t < KT0; ++t) acc = mfma16(w1[n][t], HOIST ? a1h[HOIST ? f : 0][t] : af[t * Y1F * 64], acc);
         if (pi < 2 * Y1C) {
           const int c = PCH * w + 16 * n + 4 * q16;
-          const float4 bv = bias(0, n);
+          const float4 bv = bz0[n];
           const float v0 = fmaxf(acc[0] + bv.x, 0.f), v1 = fmaxf(acc[1] + bv.y, 0.f);
           const float v2 = fmaxf(acc[2] + bv.z, 0.f), v3 = fmaxf(acc[3] + bv.w, 0.f);
           const u32x2 o = ok ? (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)} : (u32x2){0u, 0u};
@@ -470,6 +473,9 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
 #pragma unroll
         for (int t = 0; t < KT1; ++t) a2h[f][t] = *(const s16x8*)(Ab + (t * Y2F + f) * 1024 + lane * 16);
     }
+    float4 bz1[NFW];                                 // read before the pool stores
+#pragma unroll
+    for (int n = 0; n < NFW; ++n) bz1[n] = bias(1, n);
 #pragma unroll
     for (int fc = 0; fc < Y2FR; ++fc) {
       const s16x8* a0 = (const s16x8*)(Ab + fc * 1024 + lane * 16);
@@ -485,7 +491,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
           acc1 = mfma16(w2[n][t], HOIST ? a2h[HOIST ? Y2FR + fc : 0][t] : a1[t * Y2F * 64], acc1);
         }
         float vm[4];
-        const float4 b4 = bias(1, n);
+        const float4 b4 = bz1[n];
         const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
         // bf16 rounding: the values an unfused separable conv would have stored
         const u32x2 y2a = {pack_bf16(acc0[0] + bb[0], acc0[1] + bb[1]), pack_bf16(acc0[2] + bb[2], acc0[3] + bb[3])};
