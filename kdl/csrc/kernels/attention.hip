@@ -188,22 +188,45 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int nkt = (a.T + AT_KV - 1) / AT_KV;
   const int TK = nkt * AT_KV;
   const u32x4 z = {0u, 0u, 0u, 0u};
+  // Staging in chunks: each thread first issues the global loads of up to 4 K rows (2 V key
+  // pairs), then writes them to LDS -- one item per loop trip put a full global round trip per
+  // item on the critical path (~5 of them at T = 197 with 13 waves)
   // K rows (8 lanes per 128-byte row: coalesced), zero beyond T
-  for (int i = tid; i < TK * 8; i += nth) {
-    const int k = i >> 3, kc = i & 7;
-    *(u32x4*)(ks + k * AT_ROW + kc * 8) = k < a.T ? *(const u32x4*)(base + (long)k * ld + koff + kc * 8) : z;
+  for (int i0 = tid; i0 < TK * 8; i0 += 4 * nth) {
+    u32x4 kv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * nth, k = i >> 3, kc = i & 7;
+      kv[u] = i < TK * 8 && k < a.T ? *(const u32x4*)(base + (long)k * ld + koff + kc * 8) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * nth;
+      if (i < TK * 8) *(u32x4*)(ks + (i >> 3) * AT_ROW + (i & 7) * 8) = kv[u];
+    }
   }
   // V^T as packed key pairs: item = (chunk, key pair), pair fastest -> conflict-free b32 writes
-  for (int i = tid; i < (TK / 2) * 8; i += nth) {
-    const int kp = i % (TK / 2), ch = i / (TK / 2);
-    const int k0 = 2 * kp;
-    const uint16_t* vb = base + (long)k0 * ld + voff + ch * 8;
-    const u32x4 v0 = k0 < a.T ? *(const u32x4*)vb : z;
-    const u32x4 v1 = k0 + 1 < a.T ? *(const u32x4*)(vb + ld) : z;
+  for (int i0 = tid; i0 < (TK / 2) * 8; i0 += 2 * nth) {
+    u32x4 v0[2], v1[2];
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      *(uint32_t*)(vt + (ch * 8 + 2 * d) * AW_VROW + k0) = (v0[d] & 0xffffu) | (v1[d] << 16);
-      *(uint32_t*)(vt + (ch * 8 + 2 * d + 1) * AW_VROW + k0) = (v0[d] >> 16) | (v1[d] & 0xffff0000u);
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * nth;
+      const int kp = i % (TK / 2), ch = i / (TK / 2), k0 = 2 * kp;
+      const bool in = i < (TK / 2) * 8;
+      const uint16_t* vb = base + (long)k0 * ld + voff + ch * 8;
+      v0[u] = in && k0 < a.T ? *(const u32x4*)vb : z;
+      v1[u] = in && k0 + 1 < a.T ? *(const u32x4*)(vb + ld) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * nth;
+      if (i >= (TK / 2) * 8) continue;
+      const int kp = i % (TK / 2), ch = i / (TK / 2), k0 = 2 * kp;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        *(uint32_t*)(vt + (ch * 8 + 2 * d) * AW_VROW + k0) = (v0[u][d] & 0xffffu) | (v1[u][d] << 16);
+        *(uint32_t*)(vt + (ch * 8 + 2 * d + 1) * AW_VROW + k0) = (v0[u][d] >> 16) | (v1[u][d] & 0xffff0000u);
+      }
     }
   }
   const int qi = wave * 16 + c;
