@@ -320,7 +320,8 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     // 2k = R+1) or k+1 (PT 0: x row 2k+2 = R+2; x row 2k is no longer in the ring)
     {
       const uint32_t* wq = dwl + (t1 * 4 + q16) * 40;
-      u32x2 dv[U1W][2];                              // DWM: every unit's outputs, stored after the loop
+      u32x2 dv[U1W][2];                              // every unit's outputs, stored after the loop
+      s16x8 vv[U1W];
       uint8_t* ddst[U1W];
 #pragma unroll
       for (int i = 0; i < U1W; ++i) ddst[i] = nullptr;
@@ -348,14 +349,22 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             auto tap = [&](int ti) {
               return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * XROW + (ti % 3) * 16);
             };
-            *(s16x8*)(Ab + (t1 * Y1F + f) * 1024 + lane * 16) = eb_dw8<RELU1>(tap, wq);
+            // 1-slice configs store after the loop (see eb_dw_store); block3's register-bound
+            // config stores at once (the deferred form spilled 67 VGPRs there)
+            if constexpr (NFW == 1 && OCC == 1) {
+              vv[i] = eb_dw8<RELU1>(tap, wq);
+              ddst[i] = Ab + (t1 * Y1F + f) * 1024 + lane * 16;
+            } else {
+              *(s16x8*)(Ab + (t1 * Y1F + f) * 1024 + lane * 16) = eb_dw8<RELU1>(tap, wq);
+            }
           }
         }
       }
-      if constexpr (DWM) {
 #pragma unroll
-        for (int i = 0; i < U1W; ++i)
-          if (ddst[i]) eb_dw_store(ddst[i], lane, dv[i]);
+      for (int i = 0; i < U1W; ++i) {
+        if (!ddst[i]) continue;
+        if constexpr (DWM) eb_dw_store(ddst[i], lane, dv[i]);
+        else *(s16x8*)ddst[i] = vv[i];
       }
     }
     if (PT == 1 ? mode == 2 : mode >= 1) {           // residual 1x1/2 conv of its pooled row
@@ -425,6 +434,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     {
       const uint32_t* wq = dwl + ((KT0 + t2) * 4 + q16) * 40;
       u32x2 dv2[U2W][2];
+      s16x8 vv2[U2W];
       uint8_t* ddst2[U2W];
 #pragma unroll
       for (int i = 0; i < U2W; ++i) ddst2[i] = nullptr;
@@ -450,14 +460,20 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             auto tap = [&](int ti) {
               return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * Y1ROW + (ti % 3) * 16);
             };
-            *(s16x8*)(Ab + (t2 * Y2F + f) * 1024 + lane * 16) = eb_dw8<false>(tap, wq);
+            if constexpr (NFW == 1 && OCC == 1) {
+              vv2[i] = eb_dw8<false>(tap, wq);
+              ddst2[i] = Ab + (t2 * Y2F + f) * 1024 + lane * 16;
+            } else {
+              *(s16x8*)(Ab + (t2 * Y2F + f) * 1024 + lane * 16) = eb_dw8<false>(tap, wq);
+            }
           }
         }
       }
-      if constexpr (DWM) {
 #pragma unroll
-        for (int i = 0; i < U2W; ++i)
-          if (ddst2[i]) eb_dw_store(ddst2[i], lane, dv2[i]);
+      for (int i = 0; i < U2W; ++i) {
+        if (!ddst2[i]) continue;
+        if constexpr (DWM) eb_dw_store(ddst2[i], lane, dv2[i]);
+        else *(s16x8*)ddst2[i] = vv2[i];
       }
     }
     __syncthreads();                                 // B3: A (y2) complete
