@@ -68,11 +68,12 @@ def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
 
 
 def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, margin: float = 0.002,
-               log=print, only: set | None = None, tie: str | None = None, verbose: bool = False) -> dict:
+               log=print, only: set | None = None, tie: str | None = None, verbose: bool = False,
+               steps_re: str | None = None) -> dict:
     """``only``: challenge the incumbents with these tile configs only (e.g. newly added ids).
     ``tie``: regex; steps whose names are equal once it is replaced by '*' move together (the
     12 identical encoder layers of a ViT: one layer's few-us win sits inside the margin, the
-    same tile on all twelve does not)."""
+    same tile on all twelve does not). ``steps_re``: regex; only matching steps are tuned."""
     import re
     table = dict(eng.tuning())
     eng.apply_tuning(table)
@@ -84,6 +85,8 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
         steps = _steps_of(eng)
         groups: dict[str, list] = {}
         for st in steps:
+            if steps_re and not re.search(steps_re, st.name):
+                continue
             groups.setdefault(re.sub(tie, "*", st.name) if tie else st.name, []).append(st)
         for i, (gname, members) in enumerate(groups.items()):
             step, name = members[0], gname
@@ -144,6 +147,7 @@ def main(argv=None) -> int:
     ap.add_argument("--verbose", action="store_true", help="log every challenger's graph time")
     ap.add_argument("--margin", type=float, default=0.002, help="relative win a challenger must show (screen and A/B)")
     ap.add_argument("--tie", default=None, help=r"regex, e.g. 'encoder_layer_\d+': tune matching layers together")
+    ap.add_argument("--steps-re", default=None, help="regex: tune only the matching steps")
     a = ap.parse_args(argv)
     from . import registry
     from .tuning import tuning_path
@@ -174,7 +178,7 @@ def main(argv=None) -> int:
     t0 = time.time()
     only = {int(c) for c in a.cfgs.split(",")} if a.cfgs else None
     table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only,
-                       tie=a.tie, verbose=a.verbose, margin=a.margin)
+                       tie=a.tie, verbose=a.verbose, margin=a.margin, steps_re=a.steps_re)
     Path(a.out).write_text(json.dumps(table, indent=1))
     print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
     return 0
