@@ -38,9 +38,7 @@ namespace kdl {
 enum { MODE_PW = 0, MODE_CONV = 1, MODE_DW = 2 };
 
 // DT: element type (common.h Elt): 0 bf16, 1 fp16 (MODE_PW / MODE_CONV only)
-// RP: pooled-residual epilogue build (ConvGemmArgs.rpool; bf16 MODE_PW only) -- a separate
-// instantiation, so the other builds keep their register budget
-template <int MODE, int FM, int FN, int WGM, int WGN, int DT = 0, bool RP = false>
+template <int MODE, int FM, int FN, int WGM, int WGN, int DT = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs a) {
   using E = Elt<DT>;
   static_assert(MODE != MODE_DW || DT == 0, "the fused depthwise producer is bf16-only");
@@ -247,11 +245,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void conv_gemm_kernel(ConvGemmArgs 
   }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-byte chunks per tile row
-  if constexpr (RP) {
-    epi_rpool_tile<DT>(a.res, a.y, a.ldr, a.ldy, a.OH, a.OW, a.rH, a.rW, a.rpad, a.M, a.nstore, m0, n0, BM * CPR, CPR,
-                       smem, CS, tid, NT);
-    return;
-  }
   for (int c = tid; c < BM * CPR; c += NT) {
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
@@ -281,14 +274,6 @@ static hipError_t launch_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
   const int nM = (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
-  if constexpr (MODE == MODE_PW && DT == 0) {
-    if (a.rpool) {
-      hipLaunchKernelGGL((conv_gemm_kernel<MODE, FM, FN, WGM, WGN, DT, true>), dim3(nM * nN), dim3(64 * WGM * WGN), 0,
-                         s, a);
-      return hipGetLastError();
-    }
-  }
-  if (a.rpool) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_gemm_kernel<MODE, FM, FN, WGM, WGN, DT>), dim3(nM * nN), dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();
 }

@@ -28,8 +28,7 @@ __device__ __forceinline__ void wait_vm_barrier() {
 
 // DT: element type (common.h Elt): 0 bf16, 1 fp16. (Round 2's timing ablations of this
 // kernel -- no MFMA / no DMA / no stores / contiguous A -- are in profiles/kernel_ablations_r2.txt.)
-// RP: pooled-residual epilogue build (ConvGemmArgs.rpool; bf16 MODE_PW only)
-template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int DT = 0, bool RP = false>
+template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int DT = 0>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs a) {
   using E = Elt<DT>;
   constexpr int NW = WGM * WGN;
@@ -227,11 +226,6 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   }
   __syncthreads();
   constexpr int CPR = BN / 8;
-  if constexpr (RP) {
-    epi_rpool_tile<DT>(a.res, a.y, a.ldr, a.ldy, a.OH, a.OW, a.rH, a.rW, a.rpad, mend, a.nstore, m0, n0, BM * CPR, CPR,
-                       smem, CS, tid, 64 * NW);
-    return;
-  }
   for (int c = tid; c < BM * CPR; c += 64 * NW) {
     const int r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
@@ -288,15 +282,6 @@ static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   const int nM = a.wimg ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
   const int S = a.ksplit > 1 ? a.ksplit : 1;
   if (S > 1 && ((a.K / 32) % S != 0 || !a.ws || !a.cnt || a.wimg || S > 16)) return hipErrorInvalidValue;
-  if constexpr (MODE == 0 && DT == 0) {
-    if (a.rpool) {
-      if (a.wimg) return hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT, true>), dim3(nM * nN * S),
-                         dim3(64 * WGM * WGN), 0, s, a);
-      return hipGetLastError();
-    }
-  }
-  if (a.rpool) return hipErrorInvalidValue;
   hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT>), dim3(nM * nN * S),
                      dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();

@@ -364,12 +364,12 @@ class ConvGemmLayer:
                     ldr=ldr if ldr is not None else self.ldy,
                     K=self.K, cin=self.cin_pad, NF=self.nf(cfg), nstore=self.ldy,
                     stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out),
-                    opad=int(opad), dt=self.dt, krot=int(self.krot), **self._rpool_args(opad))
+                    opad=int(opad), dt=self.dt, krot=int(self.krot), **self._rpool_args())
 
-    def _rpool_args(self, opad: int) -> dict:
+    def _rpool_args(self) -> dict:
         if not self.rpool:
             return {}
-        assert self.mode == MODE_PW and not opad, (self.name, "pooled residual: MODE_PW GEMMs, plain output rows")
+        assert self.mode == MODE_PW and self.dt == 0, (self.name, "pooled residual: bf16 MODE_PW GEMMs only")
         rH, rW, pad = self.rpool
         return dict(rpool=1, rH=rH, rW=rW, rpad=pad)
 
