@@ -48,7 +48,6 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.ksplit = I(d, "ksplit");
   a.ws = P<float>(d, "ws");
   a.cnt = P<int>(d, "cnt");
-  a.rpool = I(d, "rpool"); a.rH = I(d, "rH"); a.rW = I(d, "rW"); a.rpad = I(d, "rpad");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {

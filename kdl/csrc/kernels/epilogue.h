@@ -42,54 +42,13 @@ __device__ __noinline__ u32x4 act_transcendental(int mode, u32x4 v) {
   return v;
 }
 
-// Pooled residual (ConvGemmArgs.rpool): TF-'same' 3x3/2 max over the un-pooled main-branch
-// output, out-of-range taps skipped, then the add -- the same bf16 operands and one rounding
-// as pool_add_rows_kernel, so the fused block tail is bit-identical to the pool_add pass it
-// replaces. The 9 loads of a window are issued together (8 channels each).
-// (Out of line, plain scalars: the GEMM epilogues that never pool keep their size.)
-template <int DT>
-__device__ __noinline__ u32x4 epi_pool_add(const uint16_t* res, int ldr, int OH, int OW, int rH, int rW,
-                                           int rpad, int m, int n, u32x4 v) {
-  using E = Elt<DT>;
-  const int OHW = OH * OW;
-  const int b = m / OHW, rem = m - b * OHW;
-  const int oh = rem / OW, ow = rem - oh * OW;
-  const int ih0 = 2 * oh - rpad, iw0 = 2 * ow - rpad;
-  const uint16_t* rb = res + (long)b * rH * rW * ldr + n;
-  u32x4 t[9];
-  bool ok[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    const int ih = ih0 + q / 3, iw = iw0 + q % 3;
-    ok[q] = (unsigned)ih < (unsigned)rH && (unsigned)iw < (unsigned)rW;
-    if (ok[q]) t[q] = *(const u32x4*)(rb + (long)(ih * rW + iw) * ldr);
-  }
-  float mx[8];
-#pragma unroll
-  for (int d = 0; d < 8; ++d) mx[d] = -INFINITY;
-#pragma unroll
-  for (int q = 0; q < 9; ++q)
-    if (ok[q]) {
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        mx[2 * d] = fmaxf(mx[2 * d], E::lo(t[q][d]));
-        mx[2 * d + 1] = fmaxf(mx[2 * d + 1], E::hi(t[q][d]));
-      }
-    }
-#pragma unroll
-  for (int d = 0; d < 4; ++d) v[d] = E::pack(mx[2 * d] + E::lo(v[d]), mx[2 * d + 1] + E::hi(v[d]));
-  return v;
-}
-
 // v: 8 bf16 / fp16 (DT) values (bias + optional pre-residual ReLU already applied) for
 // row m, cols n..n+7
 template <int DT = 0>
 __device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u32x4 v) {
   using E = Elt<DT>;
   if (a.relu_out >= 3) v = act_transcendental<DT>(a.relu_out, v);
-  if (a.rpool) {
-    v = epi_pool_add<DT>(a.res, a.ldr, a.OH, a.OW, a.rH, a.rW, a.rpad, m, n, v);
-  } else if (a.res) {
+  if (a.res) {
     const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
 #pragma unroll
     for (int d = 0; d < 4; ++d) v[d] = E::pack(E::lo(v[d]) + E::lo(rv[d]), E::hi(v[d]) + E::hi(rv[d]));

@@ -49,11 +49,6 @@ struct ConvGemmArgs {
   int ksplit;
   float* ws;
   int* cnt;
-  // pooled residual (Xception blocks 4 / 13: the block's 1x1/2 residual conv absorbs the
-  // main branch's TF-'same' 3x3/2 max-pool + add): rpool = 1 -> the residual of output row m
-  // (pixel b, oh, ow) is max over res[b][2oh-rpad+dy][2ow-rpad+dx] (dy, dx < 3, in range),
-  // res being the un-pooled [B][rH][rW][ldr] main-branch output
-  int rpool, rH, rW, rpad;
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);

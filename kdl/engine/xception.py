@@ -6,13 +6,12 @@ Walks ``kdl.models.xception.SPEC`` and lowers it to fused HIP launches:
     conv_gemm MODE_CONV  block1_conv2 3x3 + BN + ReLU (implicit GEMM)
     conv_gemm MODE_DW    every SeparableConv2D + BN (+ReLU in/out)(+residual add)
     conv_gemm MODE_PW    residual 1x1/2 convs + BN
-    conv_gemm rpool      blocks 4 and 13: the residual conv, whose epilogue max-pools the
-                         main branch (TF-'same' 3x3/2) and adds it (pool_add: KDL_POOL_EPI=0)
+    pool_add             TF-'same' 3x3/2 max-pool + residual add
     entry_block          blocks 2 and 3 (both separable convs, the pool and the residual conv)
                          as ONE persistent launch each (kdl/ops/entry_block.py; KDL_ENTRY_BLOCK)
     head_dense           GAP -> Dense(100)+ReLU -> Dense(10) logits
 
-= 42 launches per forward with the tuned table (vs ~168 unfused TF ops; split
+= 44 launches per forward with the tuned table (vs ~168 unfused TF ops; split
 separable convs count twice: depthwise + GEMM), captured into
 one hipGraph per batch bucket. All buffers are allocated once for the largest
 bucket (static memory plan); smaller buckets use prefixes of the same buffers.
@@ -54,9 +53,6 @@ class XceptionEngine(EngineBase):
         for v in filter(None, (x.strip() for x in spec.split(","))):
             blk, _, cfg = v.partition(":")
             self.fused_blocks[int(blk)] = int(cfg) if cfg else None
-        # pooled block tails (blocks 4 and 13): the residual 1x1/2 conv's epilogue does the
-        # 3x3/2 max-pool + add (KDL_POOL_EPI=0: the separate pool_add pass)
-        self.pool_epi = os.environ.get("KDL_POOL_EPI", "1") != "0"
         self.size = X.INPUT_SIZE
         self.shapes: dict[str, tuple[int, int, int]] = {}  # buffer -> (H, W, C) per image
         self._build(params)
@@ -118,26 +114,18 @@ class XceptionEngine(EngineBase):
                     self.shapes[out] = (oh, oh, s2.ldy)
                     cur, H = out, oh
                     continue
-                if not self.pool_epi:
-                    self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh)))
-                    self.shapes[rname] = (oh, oh, lay.ldy)
+                self.steps.append(Step("conv", rc.name, lay, cur, rname, geom=(H, H, oh, oh)))
+                self.shapes[rname] = (oh, oh, lay.ldy)
                 y = cur
                 for op in blk.main:
-                    slay = self._sep(p, op, dev)
+                    lay = self._sep(p, op, dev)
                     dst = f"{op.name}_out"
-                    self.steps.append(Step("conv", op.name, slay, y, dst, geom=(H, H, H, H)))
-                    self.shapes[dst] = (H, H, slay.ldy)
+                    self.steps.append(Step("conv", op.name, lay, y, dst, geom=(H, H, H, H)))
+                    self.shapes[dst] = (H, H, lay.ldy)
                     y = dst
                 C = self.shapes[y][2]
-                if self.pool_epi:
-                    # the residual conv runs last and its epilogue max-pools the main branch
-                    # (ConvGemmArgs.rpool): no pool_add pass, no residual round trip
-                    assert lay.ldy == C, (rc.name, lay.ldy, C)
-                    lay.rpool = (H, H, pt)
-                    self.steps.append(Step("conv", rc.name, lay, cur, out, res=y, geom=(H, H, oh, oh)))
-                else:
-                    self.steps.append(Step("pool", f"block{bi + 1}_pool", src=y, dst=out, res=rname,
-                                           geom=(H, H, oh, oh), extra=dict(pad=pt, C=C)))
+                self.steps.append(Step("pool", f"block{bi + 1}_pool", src=y, dst=out, res=rname,
+                                       geom=(H, H, oh, oh), extra=dict(pad=pt, C=C)))
                 self.shapes[out] = (oh, oh, C)
                 cur, H = out, oh
             elif blk.kind == "middle":

@@ -237,9 +237,6 @@ class ConvGemmLayer:
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
         # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
         self.split = False
-        # pooled residual epilogue (ConvGemmArgs.rpool): (rH, rW, pad) of the un-pooled residual
-        # operand, set by engines on a block's 1x1/2 residual conv (MODE_PW only)
-        self.rpool: tuple[int, int, int] | None = None
 
     def variants(self, W: int | None = None) -> list[tuple[bool, int]]:
         """(split, cfg) pairs valid for this layer (``W``: image width, filters the
@@ -272,7 +269,7 @@ class ConvGemmLayer:
         split = self.split if split is None else split
         cfg = self.cfg if cfg is None else cfg
         if is_blaslt(cfg):
-            assert wimg is None and not split and not self.rpool
+            assert wimg is None and not split
             self._emit_blaslt(prog, x, y, g, res, ldx, ldr, cfg, opad)
             return
         C = _lib.lib()
@@ -364,14 +361,7 @@ class ConvGemmLayer:
                     ldr=ldr if ldr is not None else self.ldy,
                     K=self.K, cin=self.cin_pad, NF=self.nf(cfg), nstore=self.ldy,
                     stride=self.stride, relu_in=int(self.relu_in), relu_out=int(self.relu_out),
-                    opad=int(opad), dt=self.dt, krot=int(self.krot), **self._rpool_args())
-
-    def _rpool_args(self) -> dict:
-        if not self.rpool:
-            return {}
-        assert self.mode == MODE_PW and self.dt == 0, (self.name, "pooled residual: bf16 MODE_PW GEMMs only")
-        rH, rW, pad = self.rpool
-        return dict(rpool=1, rH=rH, rW=rW, rpad=pad)
+                    opad=int(opad), dt=self.dt, krot=int(self.krot))
 
     def launch(self, x: torch.Tensor, y: torch.Tensor, g: Geometry, res: torch.Tensor | None = None,
                cfg: int | None = None, split: bool = False, tmp: torch.Tensor | None = None,
@@ -397,10 +387,7 @@ class ConvGemmLayer:
         else:
             assert g.OH == (g.H - 1) // self.stride + 1 and g.OW == (g.W - 1) // self.stride + 1
         if res is not None:
-            rows = g.B * self.rpool[0] * self.rpool[1] if self.rpool else g.M
-            assert res.dtype == self.dtype and res.numel() >= rows * self.ldy
-        else:
-            assert not self.rpool, (self.name, "pooled residual layer launched without its operand")
+            assert res.dtype == self.dtype and res.numel() >= g.M * self.ldy
 
 
 def pack_dw_entries(dww: torch.Tensor) -> torch.Tensor:

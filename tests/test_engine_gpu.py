@@ -82,7 +82,7 @@ def test_lane_group_matches_single_engine(xparams):
     assert lanes.slot_logits(0).abs().sum().item() == 0.0   # slot 0 untouched
 
 
-@pytest.mark.parametrize("cut", ["conv2d_2", "block7_sepconv1", "block3,block8_sepconv2"])
+@pytest.mark.parametrize("cut", ["block4_pool", "block7_sepconv1", "block3,block8_sepconv2"])
 def test_stage_pipe_matches_single_engine(xparams, cut):
     """Stage pipelining (kdl/engine/stages.py): four batches in flight on two slots,
     stage 1 of batch i+1 overlapping stage 2 of batch i with parity-double-buffered

@@ -254,41 +254,6 @@ def test_pool_add(H, C, with_res):
         assert err <= 2e-2 * ref.abs().max().item(), (kw, err)
 
 
-@pytest.mark.parametrize("cin,C,H", [(256, 728, 37), (728, 1024, 19), (128, 256, 74)])
-def test_pooled_residual_epilogue(cin, C, H):
-    """Xception block tails (blocks 4 / 13): the 1x1/2 residual conv with ConvGemmArgs.rpool
-    max-pools the un-pooled main branch in its epilogue. On every config it must equal, bit for
-    bit, the same conv followed by the pool_add pass it replaces (incl. the asymmetric 74->37
-    pad), and match the fp32 oracle."""
-    from kdl.models.layers import tf_same_pad
-    from kdl.ops.conv import is_blaslt
-    gen = torch.Generator().manual_seed(13)
-    B = 3
-    OH, pt, _ = tf_same_pad(H, 3, 2)
-    lay = _layer(MODE_PW, cin, C, gen, stride=2)
-    assert lay.ldy == round_up(C, 32)
-    g = Geometry(B, H, H, OH, OH)
-    x = _rand_act((B, H, H), lay.cin_pad, cin, gen)
-    main = _rand_act((B, H, H), lay.ldy, C, gen)
-    ref = pool_add_ref(main, conv_gemm_ref(lay, x, g).to(torch.bfloat16), B, H, H, OH, OH, lay.ldy, pt)
-    cfgs = [c for _, c in lay.variants(H) if not is_blaslt(c)]
-    assert cfgs
-    for cfg in cfgs:
-        r = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
-        two = torch.full_like(r, float("nan"))
-        lay.rpool = None
-        lay.launch(x, r, g, cfg=cfg)
-        _lib.lib().pool_add(dict(x=_lib.ptr(main), res=_lib.ptr(r), y=_lib.ptr(two), B=B, H=H, W=H, OH=OH, OW=OH,
-                                 C=lay.ldy, pad_top=pt, pad_left=pt), _lib.stream_ptr())
-        fused = torch.full_like(r, float("nan"))
-        lay.rpool = (H, H, pt)
-        lay.launch(x, fused, g, res=main, cfg=cfg)
-        torch.cuda.synchronize()
-        assert torch.equal(fused.view(torch.int16), two.view(torch.int16)), f"cfg={cfg}: fused != conv + pool_add"
-        err = (fused.float().view(-1, lay.ldy) - ref).abs().max().item()
-        assert err <= 2e-2 * ref.abs().max().item(), (cfg, err)
-
-
 def test_pool_add_batch_beyond_grid_y_limit():
     """B * OH > 65535 (a server --max_batch_size of thousands): the pixel-per-thread kernel's
     grid.y cannot hold it, so the launcher takes the 1-D row-streaming grid instead of failing."""

@@ -92,7 +92,7 @@ def test_cu_masks_are_disjoint_and_cover():
     assert sum(bin(x).count("1") for x in a + b) == 256
 
 
-def _xception_engine(fused=(), pool_epi=True):
+def _xception_engine(fused=()):
     from kdl.engine import xception as XE
     from kdl.models import xception as X
 
@@ -102,7 +102,6 @@ def _xception_engine(fused=(), pool_epi=True):
             self.max_batch, self.buckets, self.steps, self.in_kind = 1, [1], [], "u8"
             self.head, self.size, self.shapes, self._remap = X.DEFAULT_HEAD, X.INPUT_SIZE, {}, {}
             self.fused_blocks = {b: None for b in fused}
-            self.pool_epi = pool_epi
 
     p = X.init_params(seed=0)
     e = Fake(p)
@@ -158,7 +157,7 @@ def test_xception_fused_entry_block_lowering():
     assert "block2" in names and not {"conv2d", "block2_sepconv1", "block2_sepconv2", "block2_pool"} & set(names)
     st = e.steps[names.index("block2")]
     assert st.kind == "block" and st.src == "stem2" and st.dst == "block2_out" and st.geom == (147, 147, 74, 74)
-    assert len(e.steps) == len(base.steps) - 2      # conv2d, sepconv1, sepconv2 (pool in conv2d's epilogue)
+    assert len(e.steps) == len(base.steps) - 3
     assert e.shapes["block2_out"] == base.shapes["block2_out"]
     sp = _analyse(e.steps, registry.get("xception").stage_cut, scratch=["__dwtmp"])
     assert sp.boundary == ["block8_sepconv3_out"]
@@ -180,26 +179,3 @@ def test_entry_block_plan_covers_every_row_once():
                     raise AssertionError((g, i))
                 if m == WARM_Y1:
                     assert run[i + 1] == (b, s, k + 1, WARM_Y2) and run[i + 2][2:] == (k + 2, OUT)
-
-
-def test_xception_pooled_block_tails():
-    """Blocks 4 and 13 (and 2 / 3 when not fused): the residual 1x1/2 conv runs after the main
-    branch and max-pools it in its epilogue (ConvGemmLayer.rpool), replacing the pool_add step;
-    KDL_POOL_EPI=0 (pool_epi False) keeps the separate pool step."""
-    e = _xception_engine(fused=[2, 3])
-    sep = _xception_engine(fused=[2, 3], pool_epi=False)
-    names = [s.name for s in e.steps]
-    assert not [n for n in names if n.endswith("_pool")]
-    assert [n for n in (s.name for s in sep.steps) if n.endswith("_pool")] == ["block4_pool", "block13_pool"]
-    assert len(e.steps) == len(sep.steps) - 2
-    for blk, rc, H, pad in [(4, "conv2d_2", 37, 1), (13, "conv2d_3", 19, 1)]:
-        i = names.index(rc)
-        st = e.steps[i]
-        assert names[i - 1] == f"block{blk}_sepconv2"
-        assert st.res == f"block{blk}_sepconv2_out" and st.dst == f"block{blk}_out"
-        assert st.layer.rpool == (H, H, pad) and st.geom == (H, H, (H - 1) // 2 + 1, (H - 1) // 2 + 1)
-        assert e.shapes[st.dst] == sep.shapes[st.dst]
-    # the asymmetric 74 -> 37 pool (block3 unfused): leading pad 0
-    e2 = _xception_engine(fused=[2])
-    st = next(s for s in e2.steps if s.name == "conv2d_1")
-    assert st.layer.rpool == (74, 74, 0)
