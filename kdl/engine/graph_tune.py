@@ -69,17 +69,20 @@ def graph_time(eng, b: int, reps: int = 30, warm: int = 3) -> float:
 
 def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, margin: float = 0.002,
                log=print, only: set | None = None, tie: str | None = None, verbose: bool = False,
-               steps_re: str | None = None) -> dict:
+               steps_re: str | None = None, budget_s: float | None = None, save=None) -> dict:
     """``only``: challenge the incumbents with these tile configs only (e.g. newly added ids).
     ``tie``: regex; steps whose names are equal once it is replaced by '*' move together (the
     12 identical encoder layers of a ViT: one layer's few-us win sits inside the margin, the
-    same tile on all twelve does not). ``steps_re``: regex; only matching steps are tuned."""
+    same tile on all twelve does not). ``steps_re``: regex; only matching steps are tuned.
+    ``budget_s``: stop after this many seconds (the table so far is kept); ``save(table)`` is
+    called after every accepted change, so a long pass leaves its progress behind."""
     import re
     table = dict(eng.tuning())
     eng.apply_tuning(table)
     base = statistics.median(graph_time(eng, b, reps) for _ in range(3))
     log(f"start: {base * 1e3:.1f} us/forward")
     t_start = base
+    t0 = time.time()
     for p in range(passes):
         changed = 0
         steps = _steps_of(eng)
@@ -89,6 +92,9 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
                 continue
             groups.setdefault(re.sub(tie, "*", st.name) if tie else st.name, []).append(st)
         for i, (gname, members) in enumerate(groups.items()):
+            if budget_s and time.time() - t0 > budget_s:
+                log(f"  time budget ({budget_s:.0f} s) reached at {gname}: stopping")
+                break
             step, name = members[0], gname
             cur = table[step.name]
             variants = [v for v in _variants_of(eng, step) if only is None or v[1] in only]
@@ -122,11 +128,13 @@ def graph_tune(eng, b: int, passes: int = 1, reps: int = 30, confirm: int = 3, m
                     log(f"  {name:22s} {cur} -> {cand}: {ma * 1e3:8.1f} -> {mb * 1e3:8.1f} us")
                     table, base, cur = trial, mb, cand
                     changed += 1
+                    if save:
+                        save(table)
                 else:
                     base = ma
             eng.apply_tuning(table)
         log(f"pass {p}: {changed} change(s), {base * 1e3:.1f} us/forward")
-        if not changed:
+        if not changed or (budget_s and time.time() - t0 > budget_s):
             break
     eng.apply_tuning(table)
     log(f"graph tune: {t_start * 1e3:.1f} -> {base * 1e3:.1f} us/forward")
@@ -148,6 +156,7 @@ def main(argv=None) -> int:
     ap.add_argument("--margin", type=float, default=0.002, help="relative win a challenger must show (screen and A/B)")
     ap.add_argument("--tie", default=None, help=r"regex, e.g. 'encoder_layer_\d+': tune matching layers together")
     ap.add_argument("--steps-re", default=None, help="regex: tune only the matching steps")
+    ap.add_argument("--budget-s", type=float, default=None, help="stop after this many seconds")
     a = ap.parse_args(argv)
     from . import registry
     from .tuning import tuning_path
@@ -178,7 +187,8 @@ def main(argv=None) -> int:
     t0 = time.time()
     only = {int(c) for c in a.cfgs.split(",")} if a.cfgs else None
     table = graph_tune(eng, a.batch, passes=a.passes, reps=a.reps, log=lambda m: print(m, flush=True), only=only,
-                       tie=a.tie, verbose=a.verbose, margin=a.margin, steps_re=a.steps_re)
+                       tie=a.tie, verbose=a.verbose, margin=a.margin, steps_re=a.steps_re,
+                       budget_s=a.budget_s, save=lambda t: Path(a.out).write_text(json.dumps(t, indent=1)))
     Path(a.out).write_text(json.dumps(table, indent=1))
     print(f"wrote {a.out} ({time.time() - t0:.0f} s, started from {start})", flush=True)
     return 0
