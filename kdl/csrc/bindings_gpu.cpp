@@ -425,17 +425,21 @@ PYBIND11_MODULE(_C, m) {
       .def("abort", &RcclComm::abort)
       .def("async_error", &RcclComm::async_error);
   py::class_<DpLeader>(m, "DpLeader")
-      .def(py::init([](HipExecBackend* local, RcclComm* sc, RcclComm* ga, std::vector<int> buckets, double timeout_s) {
-             return new DpLeader(local, sc, ga, std::move(buckets), timeout_s);
-           }),
+      .def(py::init([](HipExecBackend* local, RcclComm* sc, RcclComm* ga, std::vector<int> buckets, double timeout_s,
+                       double ping_s) { return new DpLeader(local, sc, ga, std::move(buckets), timeout_s, ping_s); }),
            py::arg("local"), py::arg("scatter"), py::arg("gather"), py::arg("rank_buckets"), py::arg("timeout_s") = 120.0,
-           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+           py::arg("ping_s") = 0.0, py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
       .def("api_ptr", [](const DpLeader& l) { return reinterpret_cast<uintptr_t>(l.api()); })
       .def_property_readonly("world", &DpLeader::world)
       .def_property_readonly("steps", &DpLeader::steps)
+      .def_property_readonly("broken", &DpLeader::broken)
       .def("send_ctrl", [](DpLeader& l, int cmd, int version) {
         py::gil_scoped_release nogil;
         return l.send_ctrl(cmd, version);
+      })
+      .def("ping", [](DpLeader& l) {
+        py::gil_scoped_release nogil;
+        return l.ping();
       })
       // direct use without the executor (tests / bench): issue + complete of one slot
       .def("run", [](DpLeader& l, int slot, int bucket, int n_real) {
@@ -450,18 +454,20 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init([](HipExecBackend* local, RcclComm* sc, RcclComm* ga) { return new DpFollower(local, sc, ga); }),
            py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
       .def_property_readonly("steps", &DpFollower::steps)
-      // serve until a non-batch control word; returns (cmd, version, seq)
-      .def("run", [](DpFollower& f) {
+      // serve until DP_STOP / DP_RELOAD; returns (cmd, version, seq). Raises RuntimeError when rank 0
+      // is silent for liveness_s (it pings while idle) or a communicator failed.
+      .def("run", [](DpFollower& f, double liveness_s) {
         DpCtrl c{};
         {
           py::gil_scoped_release nogil;
-          c = f.run();
+          c = f.run(liveness_s);
         }
         return std::make_tuple(c.cmd, c.version, c.seq);
-      });
+      }, py::arg("liveness_s") = 30.0);
   m.attr("DP_STOP") = int(DP_STOP);
   m.attr("DP_BATCH") = int(DP_BATCH);
   m.attr("DP_RELOAD") = int(DP_RELOAD);
+  m.attr("DP_PING") = int(DP_PING);
 
   py::class_<Program>(m, "Program")
       .def(py::init<>())

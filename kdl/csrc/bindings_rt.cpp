@@ -12,6 +12,7 @@
 #include <sstream>
 
 #include "runtime/batcher.h"
+#include "runtime/dp_loop.h"
 #include "runtime/dp_schedule.h"
 #include "runtime/executor.h"
 #include "runtime/sstable.h"
@@ -300,6 +301,59 @@ PYBIND11_MODULE(_rt, m) {
         }
         return out;
       }, py::arg("n") = 64);
+
+  // ---- loopback data-parallel platform (runtime/dp_loop.h): the SAME leader / follower state
+  // machine as the RCCL path (runtime/dp_core.h), over threads and host memory, for CPU tests
+  m.def("loop_unique_id", &loop::unique_id);
+  py::class_<loop::Comm>(m, "LoopComm")
+      .def(py::init<const std::string&, int, int>(), py::arg("id"), py::arg("nranks"), py::arg("rank"))
+      .def_property_readonly("rank", &loop::Comm::rank)
+      .def_property_readonly("size", &loop::Comm::size)
+      .def("kill", &loop::Comm::kill)
+      .def("abort", &loop::Comm::abort)
+      .def("error", &loop::Comm::error);
+  py::class_<loop::Device>(m, "LoopDevice")
+      .def(py::init<int, int, size_t, int, int, std::vector<int>, int, int64_t>(), py::arg("rank"), py::arg("nslots"),
+           py::arg("item_bytes"), py::arg("max_batch"), py::arg("out_cols"), py::arg("buckets"), py::arg("version") = 0,
+           py::arg("latency_us") = 0)
+      .def("api_ptr", [](const loop::Device& d) { return reinterpret_cast<uintptr_t>(d.api()); })
+      .def_property_readonly("forwards", &loop::Device::forwards)
+      .def_static("logit", &loop::Device::logit);
+  py::class_<LoopDpLeader>(m, "LoopDpLeader")
+      .def(py::init([](loop::Device* local, loop::Comm* sc, loop::Comm* ga, std::vector<int> buckets, double timeout_s,
+                       double ping_s) { return new LoopDpLeader(local, sc, ga, std::move(buckets), timeout_s, ping_s); }),
+           py::arg("local"), py::arg("scatter"), py::arg("gather"), py::arg("rank_buckets"), py::arg("timeout_s") = 10.0,
+           py::arg("ping_s") = 0.0, py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def("api_ptr", [](const LoopDpLeader& l) { return reinterpret_cast<uintptr_t>(l.api()); })
+      .def_property_readonly("world", &LoopDpLeader::world)
+      .def_property_readonly("steps", &LoopDpLeader::steps)
+      .def_property_readonly("broken", &LoopDpLeader::broken)
+      .def("send_ctrl", [](LoopDpLeader& l, int cmd, int version) {
+        py::gil_scoped_release nogil;
+        return l.send_ctrl(cmd, version);
+      })
+      .def("ping", [](LoopDpLeader& l) {
+        py::gil_scoped_release nogil;
+        return l.ping();
+      });
+  py::class_<LoopDpFollower>(m, "LoopDpFollower")
+      .def(py::init([](loop::Device* local, loop::Comm* sc, loop::Comm* ga) { return new LoopDpFollower(local, sc, ga); }),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def_property_readonly("steps", &LoopDpFollower::steps)
+      // serve until DP_STOP / DP_RELOAD; returns (cmd, version, seq); raises RuntimeError when the
+      // leader is silent for liveness_s or a communicator failed
+      .def("run", [](LoopDpFollower& f, double liveness_s) {
+        DpCtrl c{};
+        {
+          py::gil_scoped_release nogil;
+          c = f.run(liveness_s);
+        }
+        return std::make_tuple(c.cmd, c.version, c.seq);
+      }, py::arg("liveness_s") = 30.0);
+  m.attr("DP_STOP") = int(DP_STOP);
+  m.attr("DP_BATCH") = int(DP_BATCH);
+  m.attr("DP_RELOAD") = int(DP_RELOAD);
+  m.attr("DP_PING") = int(DP_PING);
 
   m.attr("ST_OK") = int(ST_OK);
   m.attr("ST_DEADLINE") = int(ST_DEADLINE);

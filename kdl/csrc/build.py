@@ -46,7 +46,7 @@ GPU_SOURCES = sorted((HERE / "kernels").glob("*.hip")) + [HERE / "runtime" / "en
                                                          HERE / "runtime" / "hip_backend.cpp",
                                                          HERE / "runtime" / "comm.cpp",
                                                          HERE / "bindings_gpu.cpp"]
-RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp")] + [
+RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp")] + [
     HERE / "bindings_rt.cpp"]
 HEADERS = sorted(HERE.rglob("*.h"))
 

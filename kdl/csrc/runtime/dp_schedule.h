@@ -25,7 +25,10 @@
 
 namespace kdl {
 
-enum DpCmd : int32_t { DP_STOP = 0, DP_BATCH = 1, DP_RELOAD = 2 };
+// DP_PING: a control word with no batch (the leader's heartbeat while idle); followers re-post
+// the control receive in the same slot. A follower that sees no control word for its liveness
+// window treats the leader as dead (dp_core.h).
+enum DpCmd : int32_t { DP_STOP = 0, DP_BATCH = 1, DP_RELOAD = 2, DP_PING = 3 };
 
 struct DpCtrl {              // 32 bytes on the wire (device-side control word)
   int32_t cmd;

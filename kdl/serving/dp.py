@@ -158,10 +158,24 @@ def _comms(rank: int, world: int, device: int):
     return [C.RcclComm(i, world, rank, device) for i in ids]
 
 
+def liveness_s() -> float:
+    """A follower that hears no control word (batch, command or heartbeat) from rank 0 for this
+    long treats it as dead and exits non-zero (KDL_DP_LIVENESS_S, default 30 s)."""
+    import os
+    return float(os.environ.get("KDL_DP_LIVENESS_S", "30"))
+
+
+def ping_s() -> float:
+    """Rank 0's heartbeat period while idle (KDL_DP_PING_S, default a sixth of the liveness)."""
+    import os
+    return float(os.environ.get("KDL_DP_PING_S", str(liveness_s() / 6)))
+
+
 def follow_native(cfg, rank: int, world: int, dev: torch.device) -> int:
     """A follower's life: per model version, receive the weights (C1), build the engine and
     its graphs, join the version's communicators, then serve rank 0's steps in C++ until a
-    DP_STOP (exit) or DP_RELOAD (next version) control word."""
+    DP_STOP (exit) or DP_RELOAD (next version) control word. Every wait is bounded
+    (kdl/csrc/runtime/dp_core.h): a silent leader ends this rank with a non-zero status."""
     from ..ops import _lib
     from .backend import GPUExecutor
     C = _lib.lib()
@@ -174,7 +188,11 @@ def follow_native(cfg, rank: int, world: int, dev: torch.device) -> int:
         f = C.DpFollower(ex.backend, *comms)
         log.info("dp rank %d/%d on %s ready (native RCCL, %s, per-rank buckets %s)", rank, world, dev,
                  cfg.dp_signature, cfg.rank_buckets())
-        cmd, version, seq = f.run()
+        try:
+            cmd, version, seq = f.run(liveness_s())
+        except RuntimeError as e:       # rank 0 silent past the liveness window, or RCCL failed
+            log.error("dp rank %d: %s -- exiting so the supervisor restarts the group", rank, e)
+            return 3
         log.info("dp rank %d: %s after %d steps", rank, "reload" if cmd == C.DP_RELOAD else "stop", f.steps)
         del f, comms, ex
         torch.cuda.synchronize(dev)
@@ -185,15 +203,17 @@ def follow_native(cfg, rank: int, world: int, dev: torch.device) -> int:
 def follow(cfg, rank: int, world: int) -> int:
     """Ranks >= 1: receive the model (C1), build the DP signature's engine on this rank's
     GPU, then run rank 0's collective steps until it broadcasts stop. SIGTERM / SIGINT are
-    ignored: the launcher stops rank 0, whose stop broadcast ends this loop (a follower that
-    died first would leave rank 0's collectives hanging)."""
+    ignored: the launcher stops rank 0, whose stop broadcast ends this loop; a dead rank 0 ends
+    it through the liveness window (native path), a dead follower fails rank 0's next step within
+    KDL_DP_TIMEOUT_S."""
     import signal
     for sg in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sg, signal.SIG_IGN)
     dev = init_group(cfg, rank, world)
     if native_ok(cfg, dev):
         rc = follow_native(cfg, rank, world, dev)
-        dist.destroy_process_group()
+        if rc == 0:                     # a dead rank 0 would leave the group's teardown hanging
+            dist.destroy_process_group()
         return rc
     source = share_source(None, dev)
     sig = source.signatures[cfg.dp_signature]
@@ -245,8 +265,12 @@ def make_native_executor_class():
             with _active_lock():
                 old = _ACTIVE["leader"]
                 if old is not None:          # a newer version: followers leave the old loop first
-                    old.send_ctrl(C.DP_RELOAD, int(self.version or 0))
                     _ACTIVE["leader"] = None
+                    if old.send_ctrl(C.DP_RELOAD, int(self.version or 0)) != 0:
+                        # a follower is gone (or the old leader already failed): the group cannot
+                        # take the new version; fail the load loudly instead of hanging in C1
+                        raise RuntimeError("dp: followers did not take DP_RELOAD; the data-parallel group "
+                                           "is broken (its ranks exit on their liveness window)")
                 # C1 for this version (the initial one was shared by server.main before loading)
                 if old is not None:
                     share_source(self.runner.source, self.device_obj())
@@ -261,7 +285,7 @@ def make_native_executor_class():
             import os
             self.comms = _comms(0, self.world, self.device)
             self.leader = _lib.lib().DpLeader(be, *self.comms, self.engine_buckets(),
-                                              float(os.environ.get("KDL_DP_TIMEOUT_S", "120")))
+                                              float(os.environ.get("KDL_DP_TIMEOUT_S", "120")), ping_s())
             return self.leader
 
         def run_native(self) -> None:
@@ -270,7 +294,8 @@ def make_native_executor_class():
             finally:
                 with _active_lock():
                     if _ACTIVE["leader"] is self.leader and self.leader is not None:
-                        self.leader.send_ctrl(_lib.lib().DP_STOP, 0)    # release the followers
+                        if self.leader.send_ctrl(_lib.lib().DP_STOP, 0) != 0:    # release the followers
+                            log.warning("dp: DP_STOP not delivered; followers exit on their liveness window")
                         _ACTIVE["leader"] = None
     return DPNativeExecutor
 

@@ -103,6 +103,23 @@ def _image_payload(raw: bytes, td: dict, sig, dims: list) -> tuple[np.ndarray, i
     return arr.reshape(n, H, W, 3), n
 
 
+def route_exact_u8(s, runner, buf, n: int):
+    """The reference gateway's f32 request is exactly x / 127.5 - 1 of 8-bit pixels
+    (keras_image_helper's Xception preprocessing, /root/reference/model_server.py:18,53): serve
+    it on the uint8 signature (4x fewer bytes to stage and copy; the same logits up to the stem's
+    rounding of bf16(x) vs u8) -- and, under ``--scatter rccl``, data parallel over the node,
+    since that is the signature the DP group serves. Shared by gRPC and REST. Returns
+    (runner, payload): unchanged when the signature or the values do not qualify."""
+    sig = runner.sig
+    if sig.input_dtype != P.DT_FLOAT or sig.input_shape[1] <= 0 or NATIVE_SIGNATURE not in s.signatures:
+        return runner, buf
+    u8 = np.empty(n * sig.input_shape[1] * sig.input_shape[2] * 3, dtype=np.uint8)
+    if not _lib.rt().f32_to_u8_exact(buf, u8):
+        return runner, buf
+    METRICS.inc("kdl_f32_as_uint8_total")
+    return s.runner(NATIVE_SIGNATURE), u8
+
+
 class Servicer:
     def __init__(self, manager: ModelManager, f32_exact_u8: bool = True):
         self.m = manager
@@ -134,14 +151,8 @@ class Servicer:
                 if f != sig.output_key:
                     raise ServingError("INVALID_ARGUMENT", f"output tensor alias not found in signature: {f}")
             buf, n = _payload(raw, inputs[sig.input_key], sig)
-            if (self.f32_exact_u8 and sig.input_dtype == P.DT_FLOAT and sig.input_shape[1] > 0
-                    and NATIVE_SIGNATURE in s.signatures):
-                # the reference gateway's f32 request is exactly x / 127.5 - 1 of 8-bit pixels: serve it
-                # on the uint8 path (the same logits up to the stem's rounding of bf16(x) vs u8)
-                u8 = np.empty(n * sig.input_shape[1] * sig.input_shape[2] * 3, dtype=np.uint8)
-                if rt.f32_to_u8_exact(buf, u8):
-                    runner, buf = s.runner(NATIVE_SIGNATURE), u8
-                    METRICS.inc("kdl_f32_as_uint8_total")
+            if self.f32_exact_u8:
+                runner, buf = route_exact_u8(s, runner, buf, n)
             t1 = time.perf_counter()
             logits = runner.predict(buf, n, _deadline_us(context))
             t2 = time.perf_counter()

@@ -22,7 +22,7 @@ from google.protobuf import json_format
 from ..ops import _lib
 from . import protos as P
 from .backend import ServingError
-from .grpc_server import signature_def_map
+from .grpc_server import route_exact_u8, signature_def_map
 from .metrics import METRICS
 from .model_repo import STATE_NAMES, ModelManager
 
@@ -32,7 +32,7 @@ _HTTP = {"INVALID_ARGUMENT": 400, "NOT_FOUND": 404, "DEADLINE_EXCEEDED": 504, "U
          "RESOURCE_EXHAUSTED": 429, "UNIMPLEMENTED": 501, "INTERNAL": 500}
 
 
-def make_handler(manager: ModelManager):
+def make_handler(manager: ModelManager, f32_exact_u8: bool = True):
     class H(BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
 
@@ -112,8 +112,11 @@ def make_handler(manager: ModelManager):
                 x = np.ascontiguousarray(x)
                 dl = self.headers.get("X-Deadline-Ms")
                 deadline = int(_lib.rt().now_us() + float(dl) * 1e3) if dl else 0
+                n_img = x.shape[0]
+                if f32_exact_u8:     # same routing as gRPC (--scatter rccl serves serving_uint8 over the node)
+                    runner, x = route_exact_u8(s, runner, x, n_img)
                 t1 = time.perf_counter()
-                out = runner.predict(x, x.shape[0], deadline).tolist()
+                out = runner.predict(x, n_img, deadline).tolist()
                 t2 = time.perf_counter()
                 r = self._send(200, {"predictions": out} if rows else {"outputs": out})
                 # same per-request stage trace as the gRPC path (SURVEY.md §5 tracing)
@@ -143,8 +146,9 @@ class _ReusePortHTTPServer(ThreadingHTTPServer):
         super().server_bind()
 
 
-def start_rest_server(manager: ModelManager, host: str, port: int, reuse_port: bool = False):
-    srv = (_ReusePortHTTPServer if reuse_port else ThreadingHTTPServer)((host, port), make_handler(manager))
+def start_rest_server(manager: ModelManager, host: str, port: int, reuse_port: bool = False,
+                      f32_exact_u8: bool = True):
+    srv = (_ReusePortHTTPServer if reuse_port else ThreadingHTTPServer)((host, port), make_handler(manager, f32_exact_u8))
     srv.daemon_threads = True
     t = threading.Thread(target=srv.serve_forever, name="rest", daemon=True)
     t.start()

@@ -40,7 +40,8 @@ class ModelServer:
                                                          reuse_port=reuse, f32_exact_u8=cfg.f32_exact_u8)
         self.grpc.start()
         if cfg.rest_api_port:
-            self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port, reuse_port=reuse)
+            self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port, reuse_port=reuse,
+                                          f32_exact_u8=cfg.f32_exact_u8)
             self.rest_port = self.rest.server_address[1]
         def load():
             try:

@@ -11,7 +11,7 @@ import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "kdl" / "csrc"
-RT = [CSRC / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp")]
+RT = [CSRC / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp")]
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 # TSAN: LLVM's runtime. GCC 11's libtsan does not intercept pthread_cond_clockwait (what
@@ -68,6 +68,24 @@ def test_native_executor_under_asan_ubsan(tmp_path):
     exe = _build(tmp_path, "exec_asan", CSRC / "tests" / "exec_stress.cpp",
                  ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
     r = _run(exe, 8, 150, env={"ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(CLANG is None, reason="needs clang++ (LLVM TSAN runtime)")
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_loopback_under_tsan(tmp_path, world):
+    """The data-parallel leader/follower state machine (dp_core.h) on the loopback platform:
+    batcher + executor + leader heartbeat + follower threads + reload + a dead follower."""
+    exe = _build(tmp_path, "dp_tsan", CSRC / "tests" / "dp_loop_stress.cpp", ["-fsanitize=thread"], cxx=CLANG)
+    r = _run(exe, world, 3, 25, env={"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr
+
+
+def test_dp_loopback_under_asan_ubsan(tmp_path):
+    exe = _build(tmp_path, "dp_asan", CSRC / "tests" / "dp_loop_stress.cpp",
+                 ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
+    r = _run(exe, 4, 3, 25, env={"ASAN_OPTIONS": "detect_leaks=1"})
     assert r.returncode == 0, r.stdout + r.stderr
 
 
