@@ -152,7 +152,12 @@ class FaultInjector:
     n = the next n batches) and delays batches of executors matching ``cpu`` by 50 ms."""
 
     def __init__(self, spec: str | None = None):
-        spec = os.environ.get("KDL_FAULT_INJECT", "") if spec is None else spec
+        if spec is None:
+            spec = os.environ.get("KDL_FAULT_INJECT", "")
+            # a --procs child restarted by the launcher (KDL_CHILD_RESTARTS > 0) models a fresh
+            # process on a repaired device: the injected fault was transient unless made sticky
+            if int(os.environ.get("KDL_CHILD_RESTARTS", "0")) > 0 and os.environ.get("KDL_FAULT_INJECT_STICKY") != "1":
+                spec = ""
         self.fail: dict[str, int] = {}
         self.delay: dict[str, float] = {}
         self._lock = threading.Lock()
@@ -550,7 +555,9 @@ class NullExecutor(_Executor):
     (tools/serve_bench.py --device null)."""
 
     def __init__(self, runner, index: int = 0):
-        super().__init__(runner, f"null{index}/{runner.sig.name}")
+        # a --procs child names its GPU slot (gpu<i>:null<k>) so KDL_FAULT_INJECT can target one child
+        gi = runner.cfg.gpu_index
+        super().__init__(runner, (f"gpu{gi}:" if gi >= 0 else "") + f"null{index}/{runner.sig.name}")
         self.native = None
 
     @property

@@ -140,19 +140,121 @@ def launch_dp(argv: list[str], cfg: ServerConfig) -> int:
     return _supervise(kids, stop_first=kids[:1])
 
 
+class ProcsSupervisor:
+    """``--procs N`` launcher state: one child per GPU slot, each replaced by a FRESH process
+    (never a re-exec: the launcher itself never touches a GPU) when it dies, while the other
+    slots keep serving on the shared ports. This is per-GPU fault isolation for the topology
+    that ships (deploy/k8s: --procs=8); the reference's only resilience is the Deployment
+    controller restarting the whole pod (/root/reference/tf-serving-clothing-model-deployment.yaml:1-8).
+
+    A slot that keeps dying (more than ``max_restarts`` within ``window_s``) is a crash loop:
+    the launcher then stops everything and exits with that child's status, so k8s restarts the
+    pod. Restarts back off exponentially (``backoff_s`` doubling, capped at 30 s)."""
+
+    def __init__(self, cmd_for, n: int, max_restarts: int = 5, window_s: float = 300.0, backoff_s: float = 1.0):
+        self.cmd_for, self.n = cmd_for, n
+        self.max_restarts, self.window_s, self.backoff_s = max_restarts, window_s, backoff_s
+        self.kids: list = [None] * n
+        self.restarts: list[list[float]] = [[] for _ in range(n)]     # restart times per slot
+        self.due: list[float | None] = [None] * n                        # pending restart time
+        self.stopping = threading.Event()
+
+    def spawn(self, i: int) -> None:
+        cmd, env = self.cmd_for(i, len(self.restarts[i]))
+        self.kids[i] = subprocess.Popen(cmd, env=env)
+
+    def step(self, now: float) -> int | None:
+        """One supervision tick: replace dead children; returns an exit status to give up with."""
+        for i, k in enumerate(self.kids):
+            if self.due[i] is not None:
+                if now >= self.due[i]:
+                    self.due[i] = None
+                    self.restarts[i].append(now)
+                    self.spawn(i)
+                    log.warning("kdl launcher: GPU slot %d restarted as pid %d (restart %d)", i, self.kids[i].pid,
+                                len(self.restarts[i]))
+                continue
+            if k is None or k.poll() is None:
+                continue
+            recent = [t for t in self.restarts[i] if now - t < self.window_s]
+            if len(recent) >= self.max_restarts:
+                log.error("kdl launcher: GPU slot %d crash loop (%d restarts in %.0f s, last status %s): giving up",
+                          i, len(recent), self.window_s, k.returncode)
+                return k.returncode or 1
+            delay = min(30.0, self.backoff_s * (2 ** len(recent)))
+            log.warning("kdl launcher: GPU slot %d (pid %d) exited with status %s; the other %d slot(s) keep "
+                        "serving, replacing it in %.1f s", i, k.pid, k.returncode, self.n - 1, delay)
+            self.due[i] = now + delay
+        return None
+
+    def run(self) -> int:
+        def forward(signum, _frame):
+            self.stopping.set()
+            for k in self.kids:
+                if k is not None and k.poll() is None:
+                    k.send_signal(signum)
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            signal.signal(sig, forward)
+        for i in range(self.n):
+            self.spawn(i)
+        rc = 0
+        while not self.stopping.is_set():
+            r = self.step(time.monotonic())
+            if r is not None:
+                rc = r
+                break
+            time.sleep(0.2)
+        for k in self.kids:
+            if k is not None and k.poll() is None:
+                k.terminate()
+        for k in self.kids:
+            if k is None:
+                continue
+            try:
+                k.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                k.kill()
+        return rc
+
+
 def launch_procs(argv: list[str], cfg: ServerConfig) -> int:
     """``--procs N``: one server process per GPU on this node, all on the same gRPC / REST ports
-    (SO_REUSEPORT: the kernel spreads client connections over them). The launcher itself never
-    touches a GPU; it forwards SIGTERM / SIGINT, and when one child dies it stops the others and
-    exits with that child's status, so the pod restarts as a whole (k8s restartPolicy)."""
+    (SO_REUSEPORT: the kernel spreads client connections over them). The launcher never touches
+    a GPU; it forwards SIGTERM / SIGINT and replaces a child that dies (ProcsSupervisor). A child
+    whose devices all went unhealthy exits by itself (EXIT_NO_DEVICE) so it is replaced too."""
     if cfg.port == 0 or cfg.rest_api_port < 0:
         raise SystemExit("--procs needs fixed ports (every process binds the same one)")
     base = strip_flags(argv, ("--procs", "--gpu_index"))
-    kids = [subprocess.Popen([sys.executable, "-m", "kdl.serving", *base, "--procs=1", f"--gpu_index={i}"])
-            for i in range(cfg.procs)]
-    log.info("kdl model server: %d processes (pids %s) sharing gRPC :%d / REST :%d", cfg.procs,
-             [k.pid for k in kids], cfg.port, cfg.rest_api_port)
-    return _supervise(kids)
+
+    def cmd_for(i: int, restarts: int):
+        env = dict(os.environ, KDL_CHILD_RESTARTS=str(restarts))
+        return [sys.executable, "-m", "kdl.serving", *base, "--procs=1", f"--gpu_index={i}"], env
+    sup = ProcsSupervisor(cmd_for, cfg.procs, max_restarts=int(os.environ.get("KDL_MAX_RESTARTS", "5")),
+                          backoff_s=float(os.environ.get("KDL_RESTART_BACKOFF_S", "1")))
+    log.info("kdl model server: %d processes sharing gRPC :%d / REST :%d", cfg.procs, cfg.port, cfg.rest_api_port)
+    return sup.run()
+
+
+EXIT_NO_DEVICE = 4       # a --procs child with no healthy executor left: replace me
+
+
+def _watch_devices(srv: "ModelServer", done: threading.Event, rc: list, grace_s: float = 1.0) -> None:
+    """--procs child: once the model has served, a child whose executors all went unhealthy
+    stops accepting (closes its listening sockets) and exits EXIT_NO_DEVICE, so the launcher
+    replaces it with a fresh process instead of leaving it to fail its share of connections."""
+    served, bad_since = False, None
+    while not done.wait(0.2):
+        ok = srv.manager.ready()
+        served = served or ok
+        if not served or ok:
+            bad_since = None
+            continue
+        bad_since = bad_since or time.monotonic()
+        if time.monotonic() - bad_since >= grace_s:
+            log.error("kdl model server (GPU slot %d): no healthy device left; closing listeners and exiting %d",
+                      srv.cfg.gpu_index, EXIT_NO_DEVICE)
+            rc[0] = EXIT_NO_DEVICE
+            done.set()
 
 
 def main(argv=None) -> int:
@@ -187,6 +289,9 @@ def main(argv=None) -> int:
     done = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *_: done.set())
+    rc = [0]
+    if cfg.gpu_index >= 0 and cfg.scatter != "rccl":
+        threading.Thread(target=_watch_devices, args=(srv, done, rc), name="device-watch", daemon=True).start()
     done.wait()
-    srv.stop()
-    return 0
+    srv.stop(grace=0.5 if rc[0] else 2.0)
+    return rc[0]

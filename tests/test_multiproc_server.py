@@ -101,3 +101,111 @@ def test_sigterm_stops_every_process(two_procs):
     assert p.wait(timeout=60) == 0
     with pytest.raises(grpc.RpcError):
         _health(target)
+
+
+# ---------------------------------------------------------------- per-GPU fault isolation
+def test_supervisor_replaces_a_dead_slot_and_gives_up_on_a_crash_loop():
+    """ProcsSupervisor with stub children: slot 1 dies -> a FRESH process replaces it (slot 0
+    untouched); a slot that dies every time trips the crash-loop limit -> the launcher exits."""
+    from kdl.serving.server import ProcsSupervisor
+    spawned = []
+
+    def cmd_for(i, restarts):
+        spawned.append((i, restarts))
+        code = "import time; time.sleep(30)" if (i == 0 or restarts > 0) else "raise SystemExit(4)"
+        return [sys.executable, "-c", code], dict(os.environ)
+    sup = ProcsSupervisor(cmd_for, 2, max_restarts=3, window_s=60, backoff_s=0.05)
+    sup.spawn(0)
+    sup.spawn(1)
+    first0 = sup.kids[0].pid
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 20 and (1, 1) not in spawned:
+        assert sup.step(time.monotonic()) is None
+        time.sleep(0.05)
+    assert (1, 1) in spawned and sup.kids[0].pid == first0 and sup.kids[0].poll() is None
+    assert sup.kids[1].poll() is None                   # the replacement serves
+    for k in sup.kids:
+        k.kill()
+        k.wait()
+
+    def always_dies(i, restarts):
+        return [sys.executable, "-c", "raise SystemExit(4)"], dict(os.environ)
+    sup = ProcsSupervisor(always_dies, 1, max_restarts=2, window_s=60, backoff_s=0.01)
+    sup.spawn(0)
+    t0, rc = time.monotonic(), None
+    while rc is None and time.monotonic() - t0 < 20:
+        rc = sup.step(time.monotonic())
+        time.sleep(0.02)
+    assert rc == 4 and len(sup.restarts[0]) == 2
+
+
+def test_failed_gpu_slot_is_replaced_while_the_other_keeps_serving(tmp_path):
+    """--procs 2 on the null device, KDL_FAULT_INJECT fails every batch of GPU slot 1: its
+    executor goes unhealthy, the child closes its listeners and exits 4, the launcher starts a
+    fresh child for slot 1, every client request succeeds (retrying a broken connection, as
+    the gateway's gRPC client does), and the launcher never exits."""
+    base = tmp_path / "clothing-model"
+    (base / "1").mkdir(parents=True)
+    (base / "1" / "synthetic.json").write_text('{"seed": 0}')
+    port = _free_port()
+    logf = tmp_path / "launcher.log"
+    env = dict(os.environ, PYTHONPATH=str(ROOT), KDL_FAULT_INJECT="fail=gpu1:-1", KDL_RESTART_BACKOFF_S="0.5")
+    with open(logf, "w") as lf:
+        p = subprocess.Popen([sys.executable, "-m", "kdl.serving", "--procs=2", f"--port={port}", "--rest_api_port=0",
+                              f"--model_base_path={base}", "--device=null", "--host=127.0.0.1",
+                              "--allowed_batch_sizes=1,2,4,8"], cwd=str(ROOT), env=env,
+                             stdout=lf, stderr=subprocess.STDOUT, start_new_session=True)
+    target = f"127.0.0.1:{port}"
+    try:
+        deadline, pids = time.time() + 240, set()
+        while time.time() < deadline and len(pids) < 2:
+            try:
+                resp, pid = _health(target)
+                if resp == b"\x08\x01":
+                    pids.add(pid)
+            except grpc.RpcError:
+                pass
+            time.sleep(0.2)
+        assert len(pids) == 2
+        rng = np.random.default_rng(1)
+        ok = failed_attempts = 0
+        for k in range(40):
+            u8 = rng.integers(0, 200, (2, 299, 299, 3), dtype=np.uint8)
+            for attempt in range(20):
+                ch = grpc.insecure_channel(target, options=[("grpc.use_local_subchannel_pool", 1),
+                                                            ("grpc.max_send_message_length", -1)])
+                try:
+                    r = PredictionStub(ch).Predict(make_request(u8, signature="serving_uint8", input_key="images"),
+                                                   timeout=30)
+                    got = np.asarray(r.outputs["dense_7"].float_val, np.float32).reshape(2, 10)
+                    want = u8[:, 0, 0, 0:1].astype(np.float32) + np.arange(10, dtype=np.float32)[None]
+                    assert np.array_equal(got, want)
+                    ok += 1
+                    break
+                except grpc.RpcError:
+                    failed_attempts += 1
+                    time.sleep(0.1)
+                finally:
+                    ch.close()
+        assert ok == 40 and failed_attempts > 0      # slot 1 did fail requests before it left
+        # the replacement for slot 1 comes up as a new process; the launcher stays up
+        deadline, seen = time.time() + 120, set()
+        while time.time() < deadline and not (seen - pids):
+            try:
+                resp, pid = _health(target)
+                if resp == b"\x08\x01":
+                    seen.add(pid)
+            except grpc.RpcError:
+                pass
+            time.sleep(0.2)
+        assert seen - pids, "no replacement child answered"
+        assert p.poll() is None
+        text = logf.read_text()
+        assert "GPU slot 1" in text and "restarted" in text
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
