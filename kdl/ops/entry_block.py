@@ -61,6 +61,19 @@ def plan_steps(B: int, OH: int, OW: int, pc: int, grid: int) -> tuple[list[tuple
     return steps, off
 
 
+def fit_plan(B: int, OH: int, OW: int, pc: int, wave: int) -> tuple[list[tuple[int, int, int, int]], list[int]]:
+    """plan_steps on ``wave`` workgroups (one resident wave), or on as many whole waves as it
+    takes for every workgroup's step table to fit EB_MAX_STEPS (large buckets: batch 128 needs
+    two waves for block2). Workgroups of later waves start as earlier ones retire: the kernel
+    has no inter-workgroup synchronisation, so any grid is correct."""
+    grid = wave
+    while True:
+        steps, off = plan_steps(B, OH, OW, pc, grid)
+        if max(b - a for a, b in zip(off, off[1:])) <= MAX_STEPS or grid >= B * OH * ((OW + pc - 1) // pc):
+            return steps, off
+        grid += wave
+
+
 class EntryBlock:
     """An entry block lowered to one entry_block launch (kernel config ``cfg``)."""
 
@@ -83,7 +96,10 @@ class EntryBlock:
     def plan(self, B: int, OH: int, OW: int) -> tuple[torch.Tensor, torch.Tensor, int]:
         key = (B, OH, OW)
         if key not in self._plans:
-            steps, off = plan_steps(B, OH, OW, self.pc, self.grid or self.occ * _lib.num_cus(self.device))
+            if self.grid:                    # an explicit grid must fit as given
+                steps, off = plan_steps(B, OH, OW, self.pc, self.grid)
+            else:                            # default: resident waves of workgroups, as many as fit
+                steps, off = fit_plan(B, OH, OW, self.pc, self.occ * _lib.num_cus(self.device))
             assert max(b - a for a, b in zip(off, off[1:])) <= MAX_STEPS, "workgroup step table > EB_MAX_STEPS"
             st = torch.tensor(steps, dtype=torch.int32).reshape(-1, 4).to(self.device)
             of = torch.tensor(off, dtype=torch.int32).to(self.device)

@@ -60,3 +60,17 @@ def test_lanes_hw_queue_budget(monkeypatch):
     assert hw_queues() == 8
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "junk")
     assert hw_queues() == 4
+
+
+@pytest.mark.parametrize("B", [1, 32, 85, 96, 128, 256])
+def test_entry_block_plan_fits_the_lds_step_table_at_any_bucket(B):
+    """one wave of workgroups overflowed EB_MAX_STEPS above ~85 images; the
+    default plan adds whole waves until every workgroup's step table fits."""
+    from kdl.ops.entry_block import MAX_STEPS, OUT, fit_plan
+    for OH, pc in ((74, 15), (74, 13), (37, 13)):
+        steps, off = fit_plan(B, OH, OH, pc, 256)
+        assert max(b - a for a, b in zip(off, off[1:])) <= MAX_STEPS
+        # every (image, strip, pooled row) output item exactly once
+        outs = sorted((b, s, p) for b, s, p, m in steps if m == OUT)
+        ns = (OH + pc - 1) // pc
+        assert outs == [(b, s, p) for b in range(B) for s in range(ns) for p in range(OH)]

@@ -67,6 +67,30 @@ def test_entry_block_matches_oracle(xparams, blk, B, grid, cfg):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("B", [96, 128])
+def test_entry_block2_large_bucket_runs_in_two_waves(xparams, B):
+    """batch >= ~85 overflowed a one-wave plan's step table (EB_MAX_STEPS); the default
+    plan now adds whole waves of workgroups. The fp32 oracle runs on the GPU at this size."""
+    from kdl.ops.entry_block import EntryBlock
+    H, C0, OH, C1 = GEOM[2]
+    s1, s2, r = _layers(xparams, 2)
+    eb = EntryBlock("block2", s1, s2, r, device=DEV)
+    _, _, grid = eb.plan(B, OH, OH)
+    assert grid > torch.cuda.get_device_properties(0).multi_processor_count
+    gen = torch.Generator().manual_seed(5)
+    x = torch.relu(torch.randn(B, H, H, C0, generator=gen)).to(torch.bfloat16).to(DEV)
+    pg = {k: v.to(DEV) for k, v in xparams.items()}
+    ref = _block_oracle(pg, x.float(), 2)
+    y = torch.full((B, OH, OH, C1), float("nan"), dtype=torch.bfloat16, device=DEV)
+    eb.emit(None, x.data_ptr(), y.data_ptr(), B, H, H)
+    torch.cuda.synchronize()
+    got = y.float()
+    assert torch.isfinite(got).all()
+    err = ((got - ref).abs().max() / ref.abs().max()).item()
+    print(f"entry block2 B={B} grid={grid}: rel max err {err:.2e}")
+    assert err < 2e-2, err
+
+
 def test_entry_block_refuses_a_step_table_over_the_lds_limit(xparams):
     from kdl.ops.entry_block import EntryBlock
     s1, s2, r = _layers(xparams, 2)
