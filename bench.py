@@ -158,6 +158,10 @@ def main(argv=None) -> int:
     ap.add_argument("--egress", choices=["gather", "local"], default="gather",
                     help="gather: RCCL-gather every step's logits to rank 0 (+ D2H there); local: each rank "
                          "D2Hs its own logits (what per-GPU serving executors do)")
+    ap.add_argument("--gather-impl", choices=["native", "torch"], default="native",
+                    help="native: kdl._C.RcclComm.gather (grouped ncclSend/ncclRecv posted straight on the comm "
+                         "stream); torch: torch.distributed.gather (its NCCL process group runs the collective "
+                         "on an internal stream of its own: a fifth stream beside 2 stages + H2D + comm)")
     ap.add_argument("--force-dist", action="store_true",
                     help="take the multi-rank code path (process group, RCCL gather) even with one rank: "
                          "measures the collective overhead on a 1-GPU box")
@@ -261,8 +265,16 @@ def main(argv=None) -> int:
     cs = torch.cuda.Stream(device=dev)      # ingress H2D
     ms = torch.cuda.Stream(device=dev) if gather or not direct else None   # RCCL scatter / gather + egress D2H
     # egress D2H (one GPU); stage-pipelined engines copy out on their last stage's stream
-    # instead, so compute stages + H2D + egress stay within GPU_MAX_HW_QUEUES (4)
+    # instead. Streams per rank: 2 stages + H2D (+ the comm stream when gathering) = at most 4,
+    # GPU_MAX_HW_QUEUES. The gather is the native RCCL one (--gather-impl native), posted on the
+    # comm stream itself: torch.distributed's NCCL process group would run it on an internal
+    # stream of its own, a fifth stream sharing a hardware queue with a compute stage.
     ds = torch.cuda.Stream(device=dev) if not gather and not a.stages else None
+    rcomm = None
+    if gather and a.gather_impl == "native" and a.dist_backend == "nccl":
+        ids = [C.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        rcomm = C.RcclComm(ids[0], world, rank, local)
     E = lambda: [torch.cuda.Event() for _ in range(NS)]  # noqa: E731
     ready, scattered, drained = E(), E(), E()
     # free[j]: slot j's input and logits are final -- one event per lane (free-running
@@ -328,9 +340,17 @@ def main(argv=None) -> int:
             with torch.cuda.stream(ms):
                 for f in free[j]:
                     ms.wait_event(f)
-                dist.gather(out, list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
-                if rank == 0:
-                    d2h(out_host[j], logits_all[j], ms)
+                if rcomm is not None:       # peers' blocks only; rank 0's own leaves from its slot
+                    rcomm.gather(out.data_ptr(), logits_all[j].data_ptr(), out.numel() * out.element_size(),
+                                 ms.cuda_stream)
+                    if rank == 0:
+                        d2h(out_host[j][:B], out, ms)
+                        if world > 1:
+                            d2h(out_host[j][B:], logits_all[j][B:], ms)
+                else:
+                    dist.gather(out, list(logits_all[j].chunk(world)) if rank == 0 else None, dst=0)
+                    if rank == 0:
+                        d2h(out_host[j], logits_all[j], ms)
                 drained[j].record(ms)
                 if timed:
                     t_out[i].record(ms)
@@ -458,7 +478,7 @@ def main(argv=None) -> int:
             "config": {"model": info.description,
                        "global_batch": n_global, "seq_len": None, "image_size": S,
                        "per_gpu_batch": B, "parallelism": f"dp{world}",
-                       "ingress": a.ingress, "egress": a.egress if dist_on else "local", "hipgraph": use_graph, "lanes": a.lanes,
+                       "ingress": a.ingress, "egress": (f"{a.egress} ({a.gather_impl})" if a.egress == "gather" else a.egress) if dist_on else "local", "hipgraph": use_graph, "lanes": a.lanes,
                        **({"stages": f"{len(eng.ranges)} (cut after {a.stages})"} if a.stages else {})},
             **({"gpus_shared": True} if gpus_shared else {}),
         }

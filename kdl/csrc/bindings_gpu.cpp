@@ -168,16 +168,6 @@ EntryBlockArgs eb_args(const py::dict& d) {
     throw std::invalid_argument("entry_block: null pointer");
   return a;
 }
-BlasLtArgs blaslt_args(const py::dict& d) {
-  BlasLtArgs a{};
-  a.x = P<const void>(d, "x"); a.w = P<const void>(d, "w"); a.y = P<void>(d, "y");
-  a.res = P<const void>(d, "res"); a.bias = P<const float>(d, "bias");
-  a.M = I(d, "M"); a.N = I(d, "N"); a.K = I(d, "K");
-  a.ldx = I(d, "ldx"); a.ldy = I(d, "ldy"); a.ldr = I(d, "ldr");
-  a.act = I(d, "act"); a.dt = I(d, "dt"); a.algo = I(d, "algo");
-  a.wscale = P<const float>(d, "wscale");
-  return a;
-}
 
 FcMfmaArgs fcm_args(const py::dict& d) {
   FcMfmaArgs a{};
@@ -234,18 +224,6 @@ PYBIND11_MODULE(_C, m) {
     const auto a = conv_args(d);
     py::gil_scoped_release nogil;
     chk(conv_gemm(mode, cfg, a, S(s)), "conv_gemm");
-  });
-  // hipBLASLt GEMM node, eager (tests); returns the heuristic's algorithm count
-  m.def("blaslt", [](py::dict d, uintptr_t s) {
-    auto a = blaslt_args(d);
-    const int n = blaslt_prepare(a);
-    py::gil_scoped_release nogil;
-    chk(blaslt_run(static_cast<const BlasLtArgs&>(a), S(s)), "blaslt");
-    return n;
-  });
-  m.def("blaslt_num_algos", [](py::dict d) {
-    auto a = blaslt_args(d);
-    return blaslt_prepare(a);
   });
   m.def("conv_gemm_config", [](int cfg) {
     int bm = 0, bn = 0, th = 0;
@@ -423,7 +401,12 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("size", &RcclComm::size)
       .def("abort", &RcclComm::abort)
-      .def("async_error", &RcclComm::async_error);
+      .def("async_error", &RcclComm::async_error)
+      // gather `nbytes` per rank to rank 0 on `stream` (device pointers); no extra stream
+      .def("gather", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t nbytes, uintptr_t stream) {
+        if (rccl_gather(c, reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), nbytes, S(stream)) != 0)
+          throw std::runtime_error("rccl_gather failed");
+      });
   py::class_<DpLeader>(m, "DpLeader")
       .def(py::init([](HipExecBackend* local, RcclComm* sc, RcclComm* ga, std::vector<int> buckets, double timeout_s,
                        double ping_s) { return new DpLeader(local, sc, ga, std::move(buckets), timeout_s, ping_s); }),
@@ -473,12 +456,6 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
       .def("add_conv_gemm", [](Program& p, const std::string& name, int mode, int cfg, py::dict d) {
         Op op; op.kind = OP_CONV_GEMM; op.name = name; op.mode = mode; op.cfg = cfg; op.g = conv_args(d);
-        p.add(op);
-      })
-      .def("add_blaslt", [](Program& p, const std::string& name, py::dict d) {
-        Op op; op.kind = OP_BLASLT; op.name = name; op.bl = blaslt_args(d);
-        op.cfg = op.bl.algo;
-        blaslt_prepare(op.bl);
         p.add(op);
       })
       .def("add_stem", [](Program& p, const std::string& name, py::dict d) {

@@ -42,7 +42,6 @@ def _hipcc() -> str:
 
 
 GPU_SOURCES = sorted((HERE / "kernels").glob("*.hip")) + [HERE / "runtime" / "engine.cpp",
-                                                         HERE / "runtime" / "blaslt.cpp",
                                                          HERE / "runtime" / "hip_backend.cpp",
                                                          HERE / "runtime" / "comm.cpp",
                                                          HERE / "bindings_gpu.cpp"]
@@ -89,14 +88,14 @@ def build_gpu(force: bool = False, njobs: int = 8, verbose: bool = True) -> Path
         print(f"[kdl.build] compiling {len(jobs)} GPU source(s) for {ARCH}", flush=True)
     _compile_all(jobs, njobs)
     if force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
-        # hipBLASLt (the vendor GEMM node, runtime/blaslt.cpp): SONAME libhipblaslt.so.1, the same
-        # as the copy torch loads first (import torch precedes kdl._C), so one instance is shared;
-        # the same holds for RCCL (runtime/comm.cpp, SONAME librccl.so.1)
+        # RCCL (runtime/comm.cpp): SONAME librccl.so.1, the same as the copy torch loads first
+        # (import torch precedes kdl._C), so one instance is shared. No vendor BLAS: every GEMM
+        # of the product is a hand-written MFMA kernel (hipBLASLt lives in tools/probes/blaslt)
         # link to a temporary name, then rename: a reader (an import, a tree snapshot) sees the old
         # or the new library, never a half-written one
         tmp = out.with_name(out.name + ".tmp")
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-L/opt/rocm/lib",
-              "-lhipblaslt", "-lrccl", "-o", str(tmp)])
+              "-lrccl", "-o", str(tmp)])
         os.replace(tmp, out)
         if verbose:
             print(f"[kdl.build] linked {out.relative_to(ROOT)}", flush=True)

@@ -46,6 +46,21 @@ bool RcclComm::async_error() const {
   return ncclCommGetAsyncError(comm_, &r) != ncclSuccess || (r != ncclSuccess && r != ncclInProgress);
 }
 
+int rccl_gather(RcclComm& c, const void* send, void* recv, size_t bytes, hipStream_t stream) {
+  if (!c.get()) return -1;
+  if (c.size() == 1) return 0;
+  if (ncclGroupStart() != ncclSuccess) return -1;
+  ncclResult_t r = ncclSuccess;
+  if (c.rank() == 0) {
+    for (int p = 1; p < c.size() && r == ncclSuccess; ++p)
+      r = ncclRecv(static_cast<uint8_t*>(recv) + bytes * p, bytes, ncclUint8, p, c.get(), stream);
+  } else {
+    r = ncclSend(send, bytes, ncclUint8, 0, c.get(), stream);
+  }
+  const ncclResult_t e = ncclGroupEnd();
+  return r == ncclSuccess && e == ncclSuccess ? 0 : -1;
+}
+
 // the two class templates are instantiated once, here, for the HIP / RCCL platform
 template class DpLeaderT<HipRcclPlatform>;
 template class DpFollowerT<HipRcclPlatform>;

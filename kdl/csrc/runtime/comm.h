@@ -41,6 +41,13 @@ class RcclComm {
   int rank_, size_, device_;
 };
 
+// gather of equal-size byte blocks to rank 0 on `stream` (rank r >= 1's block -> recv + r x bytes;
+// rank 0's own block is NOT copied: the caller reads it where it is -- a 1 KB device-to-device
+// hipMemcpyAsync there cost the bench 17 % at world 1, profiles/dist_path_r5.txt), posted directly on the caller's stream: no
+// extra internal stream (torch.distributed's NCCL process group adds one per device), so a
+// stage-pipelined bench rank keeps compute stages + H2D + comm within GPU_MAX_HW_QUEUES = 4.
+int rccl_gather(RcclComm& c, const void* send, void* recv, size_t bytes, hipStream_t stream);
+
 struct HipRcclPlatform {
   using Stream = hipStream_t;
   using Event = hipEvent_t;

@@ -29,7 +29,6 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_CHSCALE: return channel_scale(op.cs, s);
     case OP_WSCALE: return weight_scale(op.ws, s);
     case OP_GEMM_F8: return gemm_f8(op.cfg, op.f8, s);
-    case OP_BLASLT: return blaslt_run(op.bl, s);
     case OP_ENTRY_BLOCK: return entry_block(op.cfg, op.eb, s);
   }
   return hipErrorInvalidValue;

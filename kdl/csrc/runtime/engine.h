@@ -12,14 +12,14 @@
 #include <vector>
 
 #include "../kernels/launch.h"
-#include "blaslt.h"
 
 namespace kdl {
 
 enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6, OP_GAP = 7, OP_FC = 8, OP_FC_MFMA = 9,
               OP_PATCHIFY = 10, OP_EMBED = 11, OP_LN = 12, OP_ATTN = 13,
               OP_DWK = 14, OP_SE = 15, OP_CHSCALE = 16, OP_GEMM_F8 = 17, OP_WSCALE = 18,
-              OP_BLASLT = 20, OP_ENTRY_BLOCK = 21 };   // 19: retired (the round-3 chained middle-flow launch)
+              OP_ENTRY_BLOCK = 21 };   // 19: retired (the round-3 chained middle-flow launch); 20: retired
+                                       // (round 5: the vendor GEMM node left the product, tools/probes/blaslt)
 
 struct Op {
   OpKind kind;
@@ -44,7 +44,6 @@ struct Op {
   WScaleArgs ws{};
   GemmF8Args f8{};
   EntryBlockArgs eb{};
-  BlasLtArgs bl{};   // OP_BLASLT: plan built at add time (blaslt_prepare)
   void* mem_ptr = nullptr;
   size_t mem_bytes = 0;
 };

@@ -18,7 +18,7 @@ from pathlib import Path
 import torch
 
 from ..ops import _lib
-from ..ops.conv import MODE_DW, ConvGemmLayer, is_blaslt, is_splitk, splitk_parts
+from ..ops.conv import MODE_DW, ConvGemmLayer, is_splitk, splitk_parts
 
 
 @dataclass
@@ -230,8 +230,7 @@ class EngineBase:
             if v is None:
                 continue
             split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
-            ok = cfg in s.layer.candidates or (is_blaslt(cfg) and (getattr(s.layer, "w_plain", None) is not None
-                                                                   or getattr(s.layer, "w8_plain", None) is not None))
+            ok = cfg in s.layer.candidates       # (ids 1000-1999, the retired hipBLASLt node, are refused)
             if is_splitk(cfg):
                 sk, base = splitk_parts(cfg)
                 ok = sk in getattr(s.layer, "ksplit", ()) and base in s.layer.candidates

@@ -63,16 +63,12 @@ class ViTEngine(EngineBase):
         if tune_file and Path(tune_file).exists():
             self.load_tuning(tune_file)
 
-    def _lin(self, name: str, w: torch.Tensor, b: torch.Tensor, relu_out: int = 0,
-             blaslt: bool = True) -> ConvGemmLayer:
-        # blaslt: hipBLASLt is a tuning candidate for the plain linears (bias, or bias + the
-        # residual as its C operand); not for mlp.0 (hipBLASLt's GELU epilogue measured 64.2 vs
-        # 58.4 us for our exact-erf one, profiles/vit_blaslt_r3.txt) or the patch embedding
-        # (writes into per-image token rows)
-        # split-K candidates: N = 768 outputs (out_proj, mlp.3) are 120 tiles of 160 x 256 at the
+    def _lin(self, name: str, w: torch.Tensor, b: torch.Tensor, relu_out: int = 0) -> ConvGemmLayer:
+        # every linear is a hand-written MFMA GEMM (the hipBLASLt candidate of rounds 3-4 is gone:
+        # tools/gemm_vs_vendor.py keeps the vendor as the yardstick). split-K candidates: N = 768 outputs (out_proj, mlp.3) are 120 tiles of 160 x 256 at the
         # bench's 6,304 token rows, under half of the 256 CUs; 2-4 splits fill the chip
         lay = ConvGemmLayer(name, MODE_PW, w.double(), b.float(), cin_pad=w.shape[1], n=w.shape[0],
-                            relu_out=relu_out, device=self.device, blaslt=blaslt and relu_out != 3,
+                            relu_out=relu_out, device=self.device,
                             ksplit=(2, 3, 4) if w.shape[0] <= 768 and w.shape[1] % 384 == 0 else ())
         lay.krot = 1    # K-rotated LDS-DMA GEMM: bf16 +0.6 % img/s, p50 -2.9 % (profiles/krot_ab.txt)
         return lay
@@ -82,7 +78,7 @@ class ViTEngine(EngineBase):
         self.ln = {}
         self.steps.append(Step("patchify", "patchify", src="input", dst="patches"))
         w = p["conv_proj.weight"].reshape(D, 3 * V.PATCH * V.PATCH)
-        self.steps.append(Step("conv", "conv_proj", self._lin("conv_proj", w, p["conv_proj.bias"], blaslt=False),
+        self.steps.append(Step("conv", "conv_proj", self._lin("conv_proj", w, p["conv_proj.bias"]),
                                "patches", "X", extra=dict(kind="patch")))
         self.cls = p["class_token"].reshape(D).float().to(dev)
         self.pos = p["encoder.pos_embedding"].reshape(self.T, D).float().contiguous().to(dev)

@@ -76,10 +76,8 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
            135: 15, 136: 11, 137: 15, 140: 8, 141: 8, 142: 8,
            143: 9, 144: 11, 145: 16, 146: 8, 147: 9}
-# ids >= BLT_BASE: the vendor GEMM node (hipBLASLt, runtime/blaslt.cpp) for plain dense linears of
-# layers built with blaslt=True; id - BLT_BASE = rank in hipBLASLt's heuristic list for the shape
-BLT_BASE = 1000
-BLT_ALGOS = 6
+# ids 1000..1999 were the hipBLASLt node (rounds 3-4); retired in round 5 -- every GEMM of the
+# product is hand-written (the vendor library stays a measuring stick: tools/gemm_vs_vendor.py)
 # ids >= SPLITK_BASE: an LDS-DMA GEMM config (16..63) with K split over ksplit workgroups per tile
 # (gemm_pipe.hip ConvGemmArgs.ksplit): SPLITK_BASE + 100 * ksplit + base id
 SPLITK_BASE = 2000
@@ -114,10 +112,6 @@ def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | No
     return False
 
 
-def is_blaslt(cfg: int) -> bool:
-    return BLT_BASE <= cfg < SPLITK_BASE
-
-
 def is_splitk(cfg: int) -> bool:
     return cfg >= SPLITK_BASE
 
@@ -133,8 +127,6 @@ def splitk_id(ksplit: int, base: int) -> int:
 
 
 def cfg_tile(cfg: int) -> tuple[int, int]:
-    if is_blaslt(cfg):          # no tile of ours: channels are stored unpadded (16-granular)
-        return 256, 16
     if is_splitk(cfg):
         cfg = splitk_parts(cfg)[1]
     fm, fn, wgm, wgn = CONFIGS[cfg]
@@ -190,14 +182,11 @@ class ConvGemmLayer:
                  cin_pad: int, n: int, stride: int = 1, dww: torch.Tensor | None = None,
                  relu_in: bool = False, relu_out: bool | int = False, device="cuda",
                  candidates: list[int] | None = None, dtype: torch.dtype = torch.bfloat16,
-                 blaslt: bool = False, ksplit: tuple = ()):
+                 ksplit: tuple = ()):
         """``dtype``: element type of the activations and packed weights, bf16 (default)
         or fp16 (MODE_PW / MODE_CONV only; ``dt`` = 1 in the launch args).
         ``ksplit``: split-K factors to offer with the LDS-DMA GEMM tiles of at most 160 rows
-        (ids >= SPLITK_BASE; for layers whose M fills few CUs: ResNet-50 layer3/4).
-        ``blaslt``: also offer the hipBLASLt GEMM node (ids >= BLT_BASE) as a variant; only
-        for a plain stride-1 pointwise linear whose epilogue is bias (+ReLU) (+residual
-        as hipBLASLt's C operand, ReLU last) -- keeps an unpacked [N][K] weight copy."""
+        (ids >= SPLITK_BASE; for layers whose M fills few CUs: ResNet-50 layer3/4)."""
         assert dtype in (torch.bfloat16, torch.float16), dtype
         assert dtype == torch.bfloat16 or mode != MODE_DW, "fused separable convs are bf16-only"
         self.dtype, self.dt = dtype, int(dtype == torch.float16)
@@ -229,11 +218,6 @@ class ConvGemmLayer:
         self.ksplit = tuple(ksplit)
         assert not self.ksplit or mode in (MODE_PW, MODE_CONV, MODE_DW), (name, "split-K: LDS-DMA GEMM lowerings only")
         self._splitk_bufs: tuple | None = None     # (fp32 partials, per-tile counters), grown on demand
-        self.w_plain = None
-        if blaslt:
-            assert mode == MODE_PW and stride == 1 and self.relu_out in (0, 1, 2, 3) and not relu_in, \
-                (name, "hipBLASLt node: plain linear, bias / ReLU / GELU / residual epilogues only")
-            self.w_plain = w_nk.to(dtype).to(device).contiguous()
         # MODE_DW lowering: fused (dw in the GEMM's A producer) or split (dw3x3
         # kernel into a scratch buffer, then the MODE_PW GEMM). Autotuned.
         self.split = False
@@ -247,8 +231,7 @@ class ConvGemmLayer:
             return [(False, c) for c in self.candidates
                     if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))] + skv
         if self.mode != MODE_DW:
-            blt = [(False, BLT_BASE + i) for i in range(BLT_ALGOS)] if self.w_plain is not None else []
-            return [(False, c) for c in self.candidates if c < SEP_BASE] + blt + skv
+            return [(False, c) for c in self.candidates if c < SEP_BASE] + skv
         # separable conv: fused configs, or the split lowering (depthwise, then a plain GEMM -- split-K too)
         return ([(False, c) for c in self.candidates
                  if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W, self.K, self.n)]
@@ -268,10 +251,6 @@ class ConvGemmLayer:
         per-image copies of the packed weights (ConvGemmArgs.wimg; LDS-DMA GEMM configs only)."""
         split = self.split if split is None else split
         cfg = self.cfg if cfg is None else cfg
-        if is_blaslt(cfg):
-            assert wimg is None and not split
-            self._emit_blaslt(prog, x, y, g, res, ldx, ldr, cfg, opad)
-            return
         C = _lib.lib()
         if self.mode == MODE_DW and split:
             assert tmp is not None, "split separable conv needs a scratch buffer"
@@ -310,26 +289,6 @@ class ConvGemmLayer:
             C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())
         else:
             prog.add_conv_gemm(self.name, self.mode, cfg, ga)
-
-    def blaslt_args(self, x: int, y: int, M: int, res: int | None = None, ldx: int | None = None,
-                    ldr: int | None = None, algo: int = 0) -> dict:
-        # relu_out 1 is ReLU BEFORE the residual add, which hipBLASLt (act after C) cannot express;
-        # relu_out 3 (GELU) maps to hipBLASLt's GELU epilogue (profiles/vit_blaslt_r3.txt: its form
-        # vs the exact-erf GELU of our kernels), no residual
-        assert self.w_plain is not None, (self.name, "layer built without blaslt=True")
-        assert not (res and self.relu_out in (1, 3)), (self.name, "activation before the residual add")
-        return dict(x=x, w=_lib.ptr(self.w_plain), y=y, res=res, bias=_lib.ptr(self.bias), M=M, N=self.n,
-                    K=self.K, ldx=ldx if ldx is not None else self.cin_pad, ldy=self.ldy,
-                    ldr=ldr if ldr is not None else self.ldy, act={0: 0, 1: 1, 2: 1, 3: 2}[self.relu_out],
-                    dt=self.dt, algo=algo)
-
-    def _emit_blaslt(self, prog, x, y, g: Geometry, res, ldx, ldr, cfg: int, opad: int) -> None:
-        assert opad == 0 and g.H == g.OH and g.W == g.OW, (self.name, "hipBLASLt node: dense rows only")
-        d = self.blaslt_args(x, y, g.M, res, ldx, ldr, cfg - BLT_BASE)
-        if prog is None:
-            _lib.lib().blaslt(d, _lib.stream_ptr())
-        else:
-            prog.add_blaslt(self.name, d)
 
     def _splitk_workspace(self, ksplit: int, cfg: int, M: int):
         """fp32 partials [ksplit][tiles][BM*BN] and zeroed per-tile counters (the last split of a tile

@@ -54,9 +54,7 @@ class F8Linear:
     split = False
 
     def __init__(self, name: str, w: torch.Tensor, b: torch.Tensor, in_scale: float, relu_out: int = 0,
-                 device="cuda", candidates: list[int] | None = None, blaslt: bool = False):
-        """``blaslt``: also offer hipBLASLt's e4m3 GEMM (ids >= conv.BLT_BASE; same e4m3 operands,
-        the per-channel scales as its outer-vector A scale; bf16 output, bias, residual as C)."""
+                 device="cuda", candidates: list[int] | None = None):
         self.name = name
         self.n, self.k = w.shape
         assert self.k % 128 == 0, (name, w.shape)
@@ -76,12 +74,9 @@ class F8Linear:
         self.colscale = torch.zeros(pad, device=device)
         self.colscale[: self.n] = (sw * self.in_scale).to(device)
         self.relu_out = relu_out
-        self.w8_plain = w8.to(device).contiguous() if blaslt and relu_out == 0 else None
 
     def variants(self, W=None):
-        from .conv import BLT_ALGOS, BLT_BASE
-        blt = [(False, BLT_BASE + i) for i in range(BLT_ALGOS)] if self.w8_plain is not None else []
-        return [(False, c) for c in self.candidates] + blt
+        return [(False, c) for c in self.candidates]
 
     def args(self, x8: int, M: int, y: int | None = None, y8: int | None = None, out_scale: float = 1.0,
              res: int | None = None, ldy: int | None = None) -> dict:
@@ -90,19 +85,8 @@ class F8Linear:
                     ldy=ldy or self.n, ldr=ldy or self.n, NF=self.nf, nstore=self.n, relu_out=self.relu_out)
 
     def emit(self, prog, cfg: int | None = None, **kw) -> None:
-        from .conv import BLT_BASE, is_blaslt
         cfg = self.cfg if cfg is None else cfg
         a = self.args(**kw)
-        if is_blaslt(cfg):
-            assert self.w8_plain is not None and a["y"] and not a["y8"], (self.name, "hipBLASLt: bf16 output only")
-            d = dict(x=a["x"], w=_lib.ptr(self.w8_plain), y=a["y"], res=a["res"], bias=a["bias"], M=a["M"],
-                     N=self.n, K=self.k, ldx=self.k, ldy=a["ldy"], ldr=a["ldr"], act=0, dt=2,
-                     wscale=a["colscale"], algo=cfg - BLT_BASE)
-            if prog is None:
-                _lib.lib().blaslt(d, _lib.stream_ptr())
-            else:
-                prog.add_blaslt(self.name, d)
-            return
         if prog is None:
             _lib.lib().gemm_f8(cfg, a, _lib.stream_ptr())
         else:

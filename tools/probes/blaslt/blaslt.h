@@ -1,3 +1,8 @@
+// TOOLS-ONLY PROBE (round 5): the hipBLASLt GEMM node that rounds 3-4 offered the engines' tuner.
+// It left kdl._C -- every GEMM of the product is a hand-written MFMA kernel -- and is kept here
+// as source for vendor comparisons (build it next to a binding of your own; the committed
+// vendor yardstick is tools/gemm_vs_vendor.py, which times torch's hipBLASLt path).
+//
 // Vendor GEMM node (hipBLASLt) for the plain dense linears of the engines.
 //
 // The task's split: hand-written MFMA kernels for the fused hot ops, hipBLASLt only for
