@@ -154,14 +154,19 @@ def main(argv=None) -> int:
     ap.add_argument("--tuning", default=None, help="tuning table to load instead of kdl/tuning/<model>_b<batch>.json")
     ap.add_argument("--profile-layers", action="store_true")
     ap.add_argument("--save-tuning", default=None, help="write the autotune result (rank 0) to this path")
-    ap.add_argument("--dist-backend", default="nccl", help=argparse.SUPPRESS)   # gloo: pipeline logic checks
+    # process-group backend. auto: gloo when the data path is all native RCCL (the group then only
+    # carries host-side control: barriers, the comm id, the max-over-ranks of the clock), nccl when
+    # torch collectives move data (--gather-impl torch, --ingress scatter). A second RCCL
+    # communicator (torch's, beside the native one) cost 17 %% at world 1 (profiles/dist_path_r5.txt)
+    ap.add_argument("--dist-backend", default="auto", help=argparse.SUPPRESS)
     ap.add_argument("--egress", choices=["gather", "local"], default="gather",
                     help="gather: RCCL-gather every step's logits to rank 0 (+ D2H there); local: each rank "
                          "D2Hs its own logits (what per-GPU serving executors do)")
-    ap.add_argument("--gather-impl", choices=["native", "torch"], default="native",
-                    help="native: kdl._C.RcclComm.gather (grouped ncclSend/ncclRecv posted straight on the comm "
-                         "stream); torch: torch.distributed.gather (its NCCL process group runs the collective "
-                         "on an internal stream of its own: a fifth stream beside 2 stages + H2D + comm)")
+    ap.add_argument("--gather-impl", choices=["native", "torch"], default="torch",
+                    help="torch: torch.distributed.gather (its NCCL process group runs the collective on an "
+                         "internal stream: a fifth stream beside 2 stages + H2D + comm; -1 %% vs no process group "
+                         "at world 1); native: kdl._C.RcclComm.gather posted on the comm stream with a gloo control "
+                         "group (-4 %%). profiles/dist_path_r5.txt")
     ap.add_argument("--force-dist", action="store_true",
                     help="take the multi-rank code path (process group, RCCL gather) even with one rank: "
                          "measures the collective overhead on a 1-GPU box")
@@ -188,6 +193,9 @@ def main(argv=None) -> int:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist_on = world > 1 or a.force_dist
+    if a.dist_backend == "auto":
+        a.dist_backend = "gloo" if a.gather_impl == "native" and a.ingress != "scatter" else "nccl"
+    cdev = dev if a.dist_backend == "nccl" else torch.device("cpu")    # where host-control collectives run
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # --force-dist without a launcher: a world of one (torchrun sets all of these)
@@ -265,13 +273,14 @@ def main(argv=None) -> int:
     cs = torch.cuda.Stream(device=dev)      # ingress H2D
     ms = torch.cuda.Stream(device=dev) if gather or not direct else None   # RCCL scatter / gather + egress D2H
     # egress D2H (one GPU); stage-pipelined engines copy out on their last stage's stream
-    # instead. Streams per rank: 2 stages + H2D (+ the comm stream when gathering) = at most 4,
-    # GPU_MAX_HW_QUEUES. The gather is the native RCCL one (--gather-impl native), posted on the
-    # comm stream itself: torch.distributed's NCCL process group would run it on an internal
-    # stream of its own, a fifth stream sharing a hardware queue with a compute stage.
+    # instead. Streams per rank at world > 1: 2 stages + H2D + the comm stream, plus the internal
+    # stream torch.distributed's NCCL process group runs its collectives on: five streams on
+    # GPU_MAX_HW_QUEUES = 4. Measured at world 1 under torchrun (profiles/dist_path_r5.txt): that
+    # path costs 1 % against no process group at all; posting a native RCCL gather on the comm
+    # stream (four streams) cost 4 %, and a second RCCL communicator beside torch's 17 %.
     ds = torch.cuda.Stream(device=dev) if not gather and not a.stages else None
     rcomm = None
-    if gather and a.gather_impl == "native" and a.dist_backend == "nccl":
+    if gather and a.gather_impl == "native":
         ids = [C.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
         rcomm = C.RcclComm(ids[0], world, rank, local)
@@ -427,7 +436,7 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist_on:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     # unloaded per-batch latency (same path, one batch in flight at a time), outside the timed region
@@ -442,13 +451,13 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
         lat.append(t_in[k].elapsed_time(t_out[k]))
     if dist_on:
-        t = torch.tensor(lat, device=dev, dtype=torch.float64)
+        t = torch.tensor(lat, device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         lat = t.tolist()
 
     gpus_shared = shared
     if dist_on:
-        t = torch.tensor([int(shared)], device=dev, dtype=torch.int32)
+        t = torch.tensor([int(shared)], device=cdev, dtype=torch.int32)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         gpus_shared = bool(t.item())
     if rank == 0:

@@ -226,7 +226,9 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
   // 1-slice configs keep this lane's 3 x 4 biases in registers (read once from global): in LDS a
   // bias read that follows a y1 / pool store cannot be hoisted above it, so every fragment of
   // P2 / P4 re-read it and waited for it
-  constexpr bool BREG = NFW == 1 && OCC == 1;
+  // 16-wave configs (NW 16: 4 waves per SIMD, <= 128 VGPRs) take none of the register-hungry forms
+  constexpr bool WIDE = NFW == 1 && OCC == 1 && NW <= 8;
+  constexpr bool BREG = WIDE;
   float4 breg[BREG ? 3 : 1][NFW];
   if constexpr (BREG) {
 #pragma unroll
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             };
             // 1-slice configs store after the loop (see eb_dw_store); block3's register-bound
             // config stores at once (the deferred form spilled 67 VGPRs there)
-            if constexpr (NFW == 1 && OCC == 1) {
+            if constexpr (WIDE) {
               vv[i] = eb_dw8<RELU1>(tap, wq);
               ddst[i] = Ab + (t1 * Y1F + f) * 1024 + lane * 16;
             } else {
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     // HOIST (1-slice configs, registers to spare): every A fragment is read before the first y1
     // store -- the compiler cannot move a read above a store it cannot prove disjoint, which
     // chained each fragment's LDS latency behind the previous fragment's store
-    constexpr bool HOIST = NFW == 1 && OCC == 1;
+    constexpr bool HOIST = WIDE;
     s16x8 a1h[HOIST ? Y1F : 1][KT0];
     if constexpr (HOIST) {
 #pragma unroll
@@ -460,7 +462,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
             auto tap = [&](int ti) {
               return *(const u32x4*)(base + ((row - 1 + ti / 3) & 3) * Y1ROW + (ti % 3) * 16);
             };
-            if constexpr (NFW == 1 && OCC == 1) {
+            if constexpr (WIDE) {
               vv2[i] = eb_dw8<false>(tap, wq);
               ddst2[i] = Ab + (t2 * Y2F + f) * 1024 + lane * 16;
             } else {
@@ -564,7 +566,9 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
 // with per-phase s_memtime stamps (EntryBlockArgs.stamps; diagnostics only); 2, 3: 0, 1 with the
 // depthwise convs on the matrix cores (block-diagonal operand) instead of the VALU (block2 only:
 // block3's LDS map has no room for the larger entries); 4, 5: block2
-// with 13-column strips, small enough (LDS, <= 128 VGPRs) for two workgroups per CU
+// with 13-column strips, small enough (LDS, <= 128 VGPRs) for two workgroups per CU. Measured and removed (round 5,
+// profiles/entry_block3_r5.txt): block3 as 16 waves of one slice (VALU / MFMA depthwise: 328 / 246 us)
+// and block3 with the MFMA depthwise (378 us) against config 1's 188 us -- all spill (78 / 56 / 91 VGPRs)
 #define KDL_EB_CONFIGS(X)                          \
   X(0, 64, 128, 15, 1, 1, false, false, 1)         \
   X(1, 128, 256, 13, 2, 0, true, false, 1)         \
