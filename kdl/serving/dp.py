@@ -54,7 +54,14 @@ def init_group(cfg, rank: int, world: int) -> torch.device:
     if use_gpu:
         dev = torch.device("cuda", rank % torch.cuda.device_count())
         torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=timeout)
+        if native_ok(cfg, dev):
+            # every per-batch byte moves on the native RCCL communicators (comm.cpp); the process
+            # group only carries control (comm ids, model metadata) and the one-time weight
+            # broadcast, on the CPU: a torch RCCL communicator beside the native ones would be a
+            # third per rank (a second one cost the bench 17 %, profiles/dist_path_r5.txt)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timeout)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=timeout)
     else:
         dev = torch.device("cpu")
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timeout)
@@ -77,7 +84,8 @@ def share_source(source, dev: torch.device):
     dist.broadcast_object_list(meta, src=0)
     m = meta[0]
     params = {k: v.float() for k, v in source.params.items()} if rank == 0 else None
-    flat = D.broadcast_params(params, m["keys"], m["shapes"], dev)
+    bdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    flat = D.broadcast_params(params, m["keys"], m["shapes"], bdev)
     flat = {k: v.to(getattr(torch, m["dtypes"][k].split(".")[-1])) for k, v in flat.items()}
     if rank == 0:
         return source
