@@ -32,6 +32,30 @@ py::dict spec_dict(const ModelSpecView& s) {
   return d;
 }
 
+// f32 compat payload -> uint8 pixels when it is EXACTLY float32(u) / 127.5 - 1 for 8-bit u (what
+// the reference gateway sends: keras_image_helper's Xception preprocessing, model_server.py:18),
+// so the request rides the uint8 path (4x fewer bytes to stage, copy and decode). False (dst
+// undefined) at the first block holding a value that is not. Branch-free and vectorized (an
+// AVX2 clone picked at load time where the CPU has it): the round-4 form called std::nearbyint
+// per element and clamped with float min/max, which kept the loop scalar -- 1.2 ms per 299x299x3
+// image, more than all the rest of a request's server time (profiles/serve_f32_exact_r5.txt).
+__attribute__((target_clones("avx2", "default"))) bool f32_to_u8_exact(const float* __restrict x,
+                                                                       uint8_t* __restrict u, size_t n) {
+  const size_t B = 4096;                 // blocks: early exit between them
+  for (size_t i0 = 0; i0 < n; i0 += B) {
+    const size_t i1 = std::min(n, i0 + B);
+    int bad = 0;
+    for (size_t i = i0; i < i1; ++i) {
+      int r = (int)((x[i] + 1.0f) * 127.5f + 0.5f);   // NaN / out of range -> INT_MIN: clamped, then mismatches
+      r = r < 0 ? 0 : r > 255 ? 255 : r;
+      bad |= (float)r / 127.5f - 1.0f != x[i];       // rebuilt exactly as the gateway computed it
+      u[i] = (uint8_t)r;
+    }
+    if (bad) return false;
+  }
+  return true;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_rt, m) {
@@ -55,35 +79,12 @@ PYBIND11_MODULE(_rt, m) {
   });
   m.def("dp_plan_shard", &dp_plan_shard);
 
-  // f32 compat payload -> uint8 pixels when it is EXACTLY float32(u) / 127.5 - 1 for 8-bit u (what
-  // the reference gateway sends: keras_image_helper's Xception preprocessing, model_server.py:18),
-  // so the request rides the uint8 path (4x fewer bytes to stage, copy and decode). False (dst
-  // undefined) at the first value that is not.
   m.def("f32_to_u8_exact", [](py::buffer src, py::buffer dst) {
     py::buffer_info si = src.request(), di = dst.request(true);
     const size_t n = (size_t)si.size * si.itemsize / 4;
     if ((size_t)di.size * di.itemsize < n) throw std::invalid_argument("f32_to_u8_exact: dst too small");
-    const float* x = static_cast<const float*>(si.ptr);
-    uint8_t* u = static_cast<uint8_t*>(di.ptr);
-    bool ok = true;
-    {
-      py::gil_scoped_release nogil;
-      const size_t B = 4096;               // blocks: branch-free inner loop, early exit between blocks
-      for (size_t i0 = 0; i0 < n && ok; i0 += B) {
-        const size_t i1 = std::min(n, i0 + B);
-        int bad = 0;
-        for (size_t i = i0; i < i1; ++i) {
-          const float v = (x[i] + 1.0f) * 127.5f;
-          const float r = std::nearbyint(v);
-          const float c = std::min(std::max(r, 0.0f), 255.0f);
-          const float back = c / 127.5f - 1.0f;
-          bad |= back != x[i];
-          u[i] = (uint8_t)c;
-        }
-        ok = bad == 0;
-      }
-    }
-    return ok;
+    py::gil_scoped_release nogil;
+    return f32_to_u8_exact(static_cast<const float*>(si.ptr), static_cast<uint8_t*>(di.ptr), n);
   });
   m.attr("DP_CTRL_BYTES") = int(sizeof(DpCtrl));
 
