@@ -152,6 +152,16 @@ __device__ __forceinline__ void eb_dw_store(uint8_t* dst, int lane, const u32x2 
   for (int g = 0; g < 2; ++g) *(u32x2*)(dst + (p16 + 16 * (2 * g + par)) * 16 + 8 * (kb & 1)) = out[g];
 }
 
+// workgroup barrier for LDS hand-offs only: LDS-scoped release / acquire fences around s_barrier, so
+// the compiler orders LDS accesses around it and emits only lgkmcnt(0). __syncthreads() (a fence over
+// every address space) lowers to s_waitcnt vmcnt(0) lgkmcnt(0) + s_barrier, which drained the next
+// step's x-row LDS-DMA at the first phase barrier after its issue (B2) instead of at B0
+__device__ __forceinline__ void eb_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ s16x8 eb_frag(const uint16_t* wp, int nf, int kt, int t, int lane) {
   return *(const s16x8*)(wp + ((long)(nf * kt + t) * 64 + lane) * 8);
 }
@@ -381,7 +391,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
         if (PT == 1) acco[n] = acc;
       }
     }
-    __syncthreads();                                 // B1: A (y1) complete; x ring free for the next DMA
+    eb_lds_barrier();                                // B1: A (y1) complete; x ring free for the next DMA
     stamp(q, 1);
 
     if (st_pend) {
@@ -428,7 +438,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
         }
       }
     }
-    __syncthreads();                                 // B2: y1 rows R+2, R+3 written; A free
+    eb_lds_barrier();                                // B2: y1 rows R+2, R+3 written; A free
     stamp(q, 2);
 
     if (mode == 0) continue;                         // warm-up 1: y1 only
@@ -478,7 +488,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
         else *(s16x8*)ddst2[i] = vv2[i];
       }
     }
-    __syncthreads();                                 // B3: A (y2) complete
+    eb_lds_barrier();                                // B3: A (y2) complete
     stamp(q, 3);
 
     // ---- P4: GEMM2 + bias -> bf16 values; vertical max with the carried row

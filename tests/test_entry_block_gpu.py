@@ -67,14 +67,14 @@ def test_entry_block_matches_oracle(xparams, blk, B, grid, cfg):
     assert err < 2e-2, err
 
 
-@pytest.mark.parametrize("B", [96, 128])
-def test_entry_block2_large_bucket_runs_in_two_waves(xparams, B):
+@pytest.mark.parametrize("B,cfg", [(96, 2), (128, 2), (128, 0)])
+def test_entry_block2_large_bucket_runs_in_two_waves(xparams, B, cfg):
     """batch >= ~85 overflowed a one-wave plan's step table (EB_MAX_STEPS); the default
     plan now adds whole waves of workgroups. The fp32 oracle runs on the GPU at this size."""
     from kdl.ops.entry_block import EntryBlock
     H, C0, OH, C1 = GEOM[2]
     s1, s2, r = _layers(xparams, 2)
-    eb = EntryBlock("block2", s1, s2, r, device=DEV)
+    eb = EntryBlock("block2", s1, s2, r, device=DEV, cfg=cfg)
     _, _, grid = eb.plan(B, OH, OH)
     assert grid > torch.cuda.get_device_properties(0).multi_processor_count
     gen = torch.Generator().manual_seed(5)
@@ -99,11 +99,13 @@ def test_entry_block_refuses_a_step_table_over_the_lds_limit(xparams):
         eb.plan(2, 74, 74)
 
 
-def test_entry_block2_replays_bit_identical(xparams):
-    """Persistent kernel, host step table: two launches give identical bytes."""
+@pytest.mark.parametrize("cfg", [0, 2])
+def test_entry_block2_replays_bit_identical(xparams, cfg):
+    """Persistent kernel, host step table: two launches give identical bytes (an LDS / DMA ordering
+    bug would show as run-to-run noise; VALU and MFMA depthwise configs)."""
     from kdl.ops.entry_block import EntryBlock
     s1, s2, r = _layers(xparams, 2)
-    eb = EntryBlock("block2", s1, s2, r, device=DEV)
+    eb = EntryBlock("block2", s1, s2, r, device=DEV, cfg=cfg)
     gen = torch.Generator().manual_seed(5)
     x = torch.relu(torch.randn(4, 147, 147, 64, generator=gen)).to(torch.bfloat16).to(DEV)
     y1 = torch.empty((4, 74, 74, 128), dtype=torch.bfloat16, device=DEV)
