@@ -162,6 +162,15 @@ __device__ __forceinline__ void eb_lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// 16-byte global -> LDS DMA as inline asm (M0 = the wave-uniform LDS address; lane l lands at M0 + 16 l).
+// The compiler's waitcnt pass cannot tell an LDS-DMA destination from other LDS regions and drains
+// (vmcnt(0)) every in-flight DMA before some later LDS stores; asm is invisible to it. CONTRACT: the
+// caller waits for the DMA with its own vmcnt, and no compiler-tracked VMEM load is in flight across it.
+__device__ __forceinline__ void glds16_asm(const void* g, void* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
 __device__ __forceinline__ s16x8 eb_frag(const uint16_t* wp, int nf, int kt, int t, int lane) {
   return *(const s16x8*)(wp + ((long)(nf * kt + t) * 64 + lane) * 8);
 }
@@ -571,6 +580,362 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
   }
 }
 
+// ===================================================================================================
+// Warp-specialized entry block (configs 12 / 112: block2). The four dependent stages of a step
+// (dw1 -> GEMM1 -> dw2 -> GEMM2 + pool) are split between two wave roles that work on DIFFERENT steps
+// at the same time, one workgroup barrier per step:
+//   producers (waves 4-7)  iteration i:  dw1(i) -> A1[i&1]   dw2(i-2) -> A2[i&1]   (MFMA depthwise)
+//                                        + the x-row DMA of step i+1, + step i's residual input row
+//   consumers (waves 0-3)  iteration i:  GEMM1(i-1) <- A1 -> y1 ring      GEMM2(i-3) <- A2 + pool
+//                                        + residual 1x1/2 GEMM + output of step i-3
+// Waves w and w+4 share a SIMD (MI355X_MICROARCH.md: cyclic wave placement), so every SIMD pairs a
+// depthwise stream with a GEMM stream instead of running the phases one after another with every wave
+// in the same phase (the round-4 kernel: four barriers per step, ~2k cycles per phase, all of them
+// LDS-throughput bound -- profiles/entry_block_ab_r4.txt). Rings: x 8 rows (each step's DMA one
+// iteration ahead), y1 6 rows (GEMM1(i-1) writes rows R+4, R+5 of step i-2 while dw2(i-2) reads its
+// rows R..R+3), A1 / A2 double-buffered, residual rows in a 4-slot buffer (written by producers at
+// step i, read by consumers three iterations later). 13-column strips keep the map at 142 KiB
+// (pitch 32 px, no padding). A consumer wave owns 32 output channels of every GEMM (register-resident
+// weights); a producer wave owns a quarter of each step's depthwise units.
+template <int C0, int C1, int PC, int NWAV>
+struct EbwGeom {
+  static constexpr int Y2C = 2 * PC + 1, Y1C = Y2C + 2, XC = Y1C + 2;
+  static constexpr int PLP = (XC + 15) / 16 * 16, PLB = PLP * 16;
+  static constexpr int XROW = (C0 / 8) * PLB, Y1ROW = (C1 / 8) * PLB;
+  static constexpr int KT0 = C0 / 32, KT1 = C1 / 32;
+  static constexpr int Y1F = (2 * Y1C + 15) / 16, Y2FR = (Y2C + 15) / 16, Y2F = 2 * Y2FR;
+  static constexpr int NC = NWAV / 2, NP = NWAV / 2; // consumer / producer waves (w, w+4, ... share a SIMD)
+  static constexpr int CCH = C1 / NC;                // output channels per consumer wave
+  static constexpr int NSL = CCH / 16;               // 16-channel slices per consumer wave
+  static constexpr int XDMA = XROW / 1024;
+  static constexpr int XR = 8, YR = 6, RS = 4;       // x ring, y1 ring, residual slots
+  static constexpr int PCOLS = 16 * Y2FR;
+  static constexpr int A1B = KT0 * Y1F * 1024, A2B = KT1 * Y2F * 1024;
+  static constexpr int RESB = 16 * C0 * 2;           // one residual input row: 16 strided columns x C0
+  static constexpr int BYTES = XR * XROW + YR * Y1ROW + 2 * A1B + 2 * A2B + RS * RESB + NC * PCOLS * CCH * 2 +
+                               (KT0 + KT1) * 1024 + 4 * EB_MAX_STEPS;
+  static_assert(XROW % 1024 == 0 && RESB % 1024 == 0 && C0 % 32 == 0 && C1 % 64 == 0, "channel tiling");
+  static_assert(NP % KT0 == 0 && NP % KT1 == 0, "a producer's depthwise units share one k-step");
+  static_assert(BYTES <= 160 * 1024, "LDS");
+};
+
+template <int C0, int C1, int PC, int NWAV, int PT, bool RELU1, bool STAMP>
+__global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(EntryBlockArgs a) {
+  using G = EbwGeom<C0, C1, PC, NWAV>;
+  constexpr int KT0 = G::KT0, KT1 = G::KT1, PLB = G::PLB, XROW = G::XROW, Y1ROW = G::Y1ROW, XDMA = G::XDMA;
+  constexpr int Y1C = G::Y1C, Y2C = G::Y2C, XC = G::XC, PLP = G::PLP;
+  constexpr int Y1F = G::Y1F, Y2F = G::Y2F, Y2FR = G::Y2FR, PCOLS = G::PCOLS;
+  constexpr int XR = G::XR, YR = G::YR, RS = G::RS, NC = G::NC, NP = G::NP, CCH = G::CCH, NSL = G::NSL;
+  constexpr int U1 = KT0 * Y1F, U2 = KT1 * Y2F;
+  constexpr int U1W = (U1 + NP - 1) / NP, U2W = (U2 + NP - 1) / NP;
+  static_assert(PT == 1, "the residual row 2k is x row R+1 of the step (odd map size: block2)");
+  // distinct LDS objects: the compiler may reorder accesses of different regions
+  __shared__ __attribute__((aligned(16))) uint8_t s_x[XR * XROW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_y1[YR * Y1ROW];
+  __shared__ __attribute__((aligned(16))) uint8_t s_a1[2 * G::A1B];
+  __shared__ __attribute__((aligned(16))) uint8_t s_a2[2 * G::A2B];
+  __shared__ __attribute__((aligned(16))) uint8_t s_res[RS * G::RESB];
+  __shared__ __attribute__((aligned(16))) uint16_t s_pool[NC * PCOLS * CCH];
+  __shared__ __attribute__((aligned(16))) uint8_t s_dw[(KT0 + KT1) * 1024];
+  __shared__ uint32_t s_st[EB_MAX_STEPS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool consumer = w < NC;
+  const int q16 = lane >> 4, p16 = lane & 15;
+  const int H = a.H, W = a.W;
+  const int s0 = a.step_off[blockIdx.x], s1 = a.step_off[blockIdx.x + 1];
+  if (s0 >= s1 || s1 - s0 > EB_MAX_STEPS) return;
+
+  for (int i = tid; i < s1 - s0; i += 64 * NWAV) {
+    const int4 e = a.steps[s0 + i];
+    s_st[i] = (uint32_t)e.x | ((uint32_t)e.y << 8) | ((uint32_t)(e.z + 2) << 14) | ((uint32_t)e.w << 23);
+  }
+  for (int i = tid; i < (KT0 + KT1) * 64; i += 64 * NWAV) {
+    const int t = i / 64;
+    const u32x4 v = t < KT0 ? *(const u32x4*)((const uint8_t*)a.dwk1 + t * 1024 + (i % 64) * 16)
+                            : *(const u32x4*)((const uint8_t*)a.dwk2 + (t - KT0) * 1024 + (i % 64) * 16);
+    *(u32x4*)(s_dw + t * 1024 + (i % 64) * 16) = v;
+  }
+  // consumers: this wave's CCH output channels of every GEMM, register-resident
+  s16x8 w1[NSL][KT0], w2[NSL][KT1], wr[NSL][KT0];
+  float4 bz[3][NSL];
+  if (consumer) {
+#pragma unroll
+    for (int n = 0; n < NSL; ++n) {
+#pragma unroll
+      for (int t = 0; t < KT0; ++t) {
+        w1[n][t] = eb_frag(a.w1, NSL * w + n, KT0, t, lane);
+        wr[n][t] = eb_frag(a.wr, NSL * w + n, KT0, t, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < KT1; ++t) w2[n][t] = eb_frag(a.w2, NSL * w + n, KT1, t, lane);
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        bz[g][n] = *(const float4*)((g == 0 ? a.b1 : g == 1 ? a.b2 : a.br) + CCH * w + 16 * n + 4 * q16);
+    }
+  }
+  uint32_t sel[2][4];
+  {
+    const bool wv = (p16 >> 3) == (q16 & 1);
+    const int e = p16 & 7;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t pair = (2u * jp) | ((2u * jp + 1u) << 8);
+        const uint32_t val = (e & 1) ? (0x0c0cu | (pair << 16)) : (0x0c0c0000u | pair);
+        sel[jp][d] = (wv && (e >> 1) == d) ? val : 0x0c0c0c0cu;
+      }
+  }
+  __syncthreads();
+  if (tid == 0) {                                    // ring slot of each step's first x row (rows R+1..R+4)
+    int xp = 0, xs = 0;
+    for (int i = 0; i < s1 - s0; ++i) {
+      const uint32_t e = s_st[i];
+      if (((e >> 23) & 3) == 0) { xs = xp; xp += 4; } else { xs += 2; xp += 2; }
+      s_st[i] = e | ((uint32_t)(xs & (XR - 1)) << 25);
+    }
+  }
+  auto decode = [&](int q, int& b, int& s, int& k, int& mode, int& xs) {
+    const uint32_t e = s_st[q - s0];
+    b = e & 255; s = (e >> 8) & 63; k = (int)((e >> 14) & 511) - 2; mode = (e >> 23) & 3; xs = (e >> 25) & 7;
+  };
+  auto dma_for = [&](int q) {                        // producers only: step q's new x rows
+    int b, s, k, mode, xs;
+    decode(q, b, s, k, mode, xs);
+    const int R = 2 * k - PT, gx0 = 2 * s * PC - PT - 2;
+    const int r0 = mode == 0 ? R + 1 : R + 3, nr = mode == 0 ? 4 : 2, sl0 = mode == 0 ? xs : xs + 2;
+    for (int ii = w - NC; ii < nr * XDMA; ii += NP) {
+      const int r = r0 + ii / XDMA, d = ii % XDMA;
+      const int slot = d * 64 + lane, plane = slot / PLP, px = slot - plane * PLP;
+      const int gx = gx0 + px;
+      const bool ok = px < XC && (unsigned)r < (unsigned)H && (unsigned)gx < (unsigned)W;
+      const uint8_t* src = ok ? (const uint8_t*)(a.x + (((long)b * H + r) * W + gx) * a.ldx + plane * 8) : eb_zeros;
+      glds16_asm(src, s_x + ((sl0 + ii / XDMA) & (XR - 1)) * XROW + d * 1024);
+    }
+  };
+  auto stamp = [&](int it, int ph) {
+    if constexpr (STAMP) {
+      if (lane == 0 && (w == 0 || w == NC) && blockIdx.x < 8 && it - s0 < 64 && a.stamps)
+        a.stamps[((long)blockIdx.x * 64 + (it - s0)) * 5 + ph] = __builtin_amdgcn_s_memtime();
+    }
+  };
+
+  u32x2 carry[NSL][Y2FR];                            // consumers: y2 row R+2 of the previous step
+  __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));   // prologue loads landed (the waitcnt pass sees it)
+  eb_lds_barrier();                                  // ring-slot bits of the step words visible
+  if (!consumer) dma_for(s0);
+
+  for (int it = s0; it < s1 + 3; ++it) {
+    // producers: step `it`'s x rows (their DMA, issued last iteration) must have landed; consumers: nothing
+    if (consumer) __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4) | (0 << 8));
+    else __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
+    eb_lds_barrier();
+    stamp(it, consumer ? 0 : 2);
+    if (!consumer) {
+      // =================================================================== producers
+      const int pw = w - NC;
+      if (it + 1 < s1) dma_for(it + 1);
+      u32x2 dv1[U1W][2], dv2[U2W][2];
+      uint8_t* d1[U1W];
+      uint8_t* d2[U2W];
+#pragma unroll
+      for (int i = 0; i < U1W; ++i) d1[i] = nullptr;
+#pragma unroll
+      for (int i = 0; i < U2W; ++i) d2[i] = nullptr;
+      if (it < s1) {                                 // dw1(it) -> A1[it & 1]; residual input row of step it
+        int b, s, k, mode, xs;
+        decode(it, b, s, k, mode, xs);
+        const int t1 = pw % KT0;
+        uint8_t* const A1 = s_a1 + (it & 1) * G::A1B;
+#pragma unroll
+        for (int i = 0; i < U1W; ++i) {
+          const int u = pw + NP * i;
+          if (u < U1) {
+            const int f = u / KT0;
+            int pi = 16 * f + p16;
+            pi = pi < 2 * Y1C ? pi : 2 * Y1C - 1;
+            const int rr = pi >= Y1C, col = pi - rr * Y1C;
+            const uint8_t* base = s_x + (4 * t1 + (q16 & 1)) * PLB + col * 16;
+            auto tap = [&](int g, int ti) {
+              return *(const u32x4*)(base + 2 * g * PLB + ((xs + rr + ti / 3) & (XR - 1)) * XROW + (ti % 3) * 16);
+            };
+            auto ent = [&](int g) {
+              return *(const u32x4*)(s_dw + t1 * 1024 + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
+            };
+            eb_dw_mfma_vals<RELU1>(tap, ent, lane, sel, dv1[i]);
+            d1[i] = A1 + (t1 * Y1F + f) * 1024;
+            if constexpr (NWAV > 8) {                  // 128-VGPR builds: store at once (no deferral)
+              eb_dw_store(d1[i], lane, dv1[i]);
+              d1[i] = nullptr;
+            }
+          }
+        }
+        if (mode == 2) {                             // x row 2k = R + 1 (slot xs), 16 strided columns, C0 channels
+          uint8_t* const rs = s_res + (it & (RS - 1)) * G::RESB;
+          const int xcol = min(2 * p16 + PT + 2, XC - 1);   // lanes p16 >= PC: unused columns (clamped)
+          for (int c = q16 + 4 * pw; c < C0 / 8; c += 4 * NP)   // 16-B chunk c of every column
+            *(u32x4*)(rs + (c * 16 + p16) * 16) = *(const u32x4*)(s_x + xs * XROW + c * PLB + xcol * 16);
+        }
+      }
+      if (it - 2 >= s0 && it - 2 < s1) {            // dw2(it - 2) -> A2[it & 1]
+        int b, s, k, mode, xs;
+        decode(it - 2, b, s, k, mode, xs);
+        if (mode >= 1) {
+          const int R = 2 * k - PT, t2 = pw % KT1;
+          uint8_t* const A2 = s_a2 + (it & 1) * G::A2B;
+#pragma unroll
+          for (int i = 0; i < U2W; ++i) {
+            const int u = pw + NP * i;
+            if (u < U2) {
+              const int f = u / KT1;
+              const int rr = f / Y2FR, col = (f % Y2FR) * 16 + p16;
+              const int row = R + 1 + rr;
+              const uint8_t* base = s_y1 + (4 * t2 + (q16 & 1)) * PLB + col * 16;
+              auto tap = [&](int g, int ti) {
+                const int yr = row - 1 + ti / 3;
+                return *(const u32x4*)(base + 2 * g * PLB + ((yr % YR + YR) % YR) * Y1ROW + (ti % 3) * 16);
+              };
+              auto ent = [&](int g) {
+                return *(const u32x4*)(s_dw + (KT0 + t2) * 1024 + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
+              };
+              eb_dw_mfma_vals<false>(tap, ent, lane, sel, dv2[i]);
+              d2[i] = A2 + (t2 * Y2F + f) * 1024;
+              if constexpr (NWAV > 8) {
+                eb_dw_store(d2[i], lane, dv2[i]);
+                d2[i] = nullptr;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < U1W; ++i)
+        if (d1[i]) eb_dw_store(d1[i], lane, dv1[i]);
+#pragma unroll
+      for (int i = 0; i < U2W; ++i)
+        if (d2[i]) eb_dw_store(d2[i], lane, dv2[i]);
+      stamp(it, 3);
+    } else {
+      // =================================================================== consumers
+      if (it - 1 >= s0 && it - 1 < s1) {             // GEMM1(it - 1) <- A1[(it - 1) & 1] -> y1 ring
+        int b, s, k, mode, xs;
+        decode(it - 1, b, s, k, mode, xs);
+        const int R = 2 * k - PT, pc0 = s * PC;
+        const uint8_t* const A1 = s_a1 + ((it - 1) & 1) * G::A1B;
+#pragma unroll
+        for (int f = 0; f < Y1F; ++f) {
+          const int pi = 16 * f + p16;
+          const int rr = pi >= Y1C, col = pi - rr * Y1C;
+          const int row = R + 2 + rr, gcol = 2 * pc0 - PT - 1 + col;
+          const bool ok = (unsigned)row < (unsigned)H && (unsigned)gcol < (unsigned)W;
+          s16x8 af[KT0];
+#pragma unroll
+          for (int t = 0; t < KT0; ++t) af[t] = *(const s16x8*)(A1 + (t * Y1F + f) * 1024 + lane * 16);
+#pragma unroll
+          for (int n = 0; n < NSL; ++n) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < KT0; ++t) acc = mfma16(w1[n][t], af[t], acc);
+            if (pi < 2 * Y1C) {
+              const int c = CCH * w + 16 * n + 4 * q16;
+              const float4 bv = bz[0][n];
+              const float v0 = fmaxf(acc[0] + bv.x, 0.f), v1 = fmaxf(acc[1] + bv.y, 0.f);
+              const float v2 = fmaxf(acc[2] + bv.z, 0.f), v3 = fmaxf(acc[3] + bv.w, 0.f);
+              const u32x2 o = ok ? (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)} : (u32x2){0u, 0u};
+              *(u32x2*)(s_y1 + ((row % YR + YR) % YR) * Y1ROW + (c / 8) * PLB + col * 16 + (c & 7) * 2) = o;
+            }
+          }
+        }
+      }
+      if (it - 3 >= s0 && it - 3 < s1) {             // GEMM2(it - 3) <- A2[(it - 1) & 1] + pool + residual
+        int b, s, k, mode, xs;
+        decode(it - 3, b, s, k, mode, xs);
+        if (mode >= 1) {
+          const int R = 2 * k - PT, pc0 = s * PC;
+          const uint8_t* const A2 = s_a2 + ((it - 1) & 1) * G::A2B;
+          uint16_t* const pool = s_pool + w * (PCOLS * CCH);
+          const bool r0ok = (unsigned)R < (unsigned)H && mode == 2, r1ok = (unsigned)(R + 1) < (unsigned)H;
+          const bool r2ok = (unsigned)(R + 2) < (unsigned)H;
+#pragma unroll
+          for (int fc = 0; fc < Y2FR; ++fc) {
+            const int col = fc * 16 + p16, gcol = 2 * pc0 - PT + col;
+            const bool cok = col < Y2C && (unsigned)gcol < (unsigned)W;
+            s16x8 a0[KT1], a1f[KT1];
+#pragma unroll
+            for (int t = 0; t < KT1; ++t) {
+              a0[t] = *(const s16x8*)(A2 + (t * Y2F + fc) * 1024 + lane * 16);
+              a1f[t] = *(const s16x8*)(A2 + (t * Y2F + Y2FR + fc) * 1024 + lane * 16);
+            }
+#pragma unroll
+            for (int n = 0; n < NSL; ++n) {
+              f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int t = 0; t < KT1; ++t) {
+                acc0 = mfma16(w2[n][t], a0[t], acc0);
+                acc1 = mfma16(w2[n][t], a1f[t], acc1);
+              }
+              const float4 b4 = bz[1][n];
+              const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+              const u32x2 y2a = {pack_bf16(acc0[0] + bb[0], acc0[1] + bb[1]), pack_bf16(acc0[2] + bb[2], acc0[3] + bb[3])};
+              const u32x2 y2b = {pack_bf16(acc1[0] + bb[0], acc1[1] + bb[1]), pack_bf16(acc1[2] + bb[2], acc1[3] + bb[3])};
+              float vm[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const uint32_t dc = carry[n][fc][e >> 1], da = y2a[e >> 1], db = y2b[e >> 1];
+                const float c0 = (e & 1) ? bf_hi(dc) : bf_lo(dc);
+                const float v1 = (e & 1) ? bf_hi(da) : bf_lo(da), v2 = (e & 1) ? bf_hi(db) : bf_lo(db);
+                float m = r0ok ? c0 : -INFINITY;
+                if (r1ok) m = fmaxf(m, v1);
+                if (r2ok) m = fmaxf(m, v2);
+                vm[e] = cok ? m : -INFINITY;
+              }
+              carry[n][fc] = y2b;
+              if (mode == 2)
+                *(u32x2*)(pool + col * CCH + 16 * n + 4 * q16) = (u32x2){pack_bf16(vm[0], vm[1]), pack_bf16(vm[2], vm[3])};
+            }
+          }
+          if (mode == 2) {
+            // residual 1x1/2 conv of pooled row k from the staged input row (written three iterations ago)
+            const uint8_t* const rs = s_res + ((it - 3) & (RS - 1)) * G::RESB;
+            f32x4 racc[NSL];
+#pragma unroll
+            for (int n = 0; n < NSL; ++n) {
+              racc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int t = 0; t < KT0; ++t)
+                racc[n] = mfma16(wr[n][t], *(const s16x8*)(rs + ((4 * t + q16) * 16 + p16) * 16), racc[n]);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own pool rows only
+            const int j = p16, gj = pc0 + j;
+            if (j < PC && gj < a.OW) {
+#pragma unroll
+              for (int n = 0; n < NSL; ++n) {
+                const uint16_t* pp = pool + (2 * j) * CCH + 16 * n + 4 * q16;
+                const float4 brv = bz[2][n];
+                const float br4[4] = {brv.x, brv.y, brv.z, brv.w};
+                const u32x2 c0 = *(const u32x2*)pp, c1 = *(const u32x2*)(pp + CCH), c2 = *(const u32x2*)(pp + 2 * CCH);
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const uint32_t d0 = c0[e >> 1], d1v = c1[e >> 1], d2v = c2[e >> 1];
+                  const float m = (e & 1) ? fmaxf(fmaxf(bf_hi(d0), bf_hi(d1v)), bf_hi(d2v))
+                                          : fmaxf(fmaxf(bf_lo(d0), bf_lo(d1v)), bf_lo(d2v));
+                  o[e] = m + bf2f(f2bf(racc[n][e] + br4[e]));
+                }
+                *(u32x2*)(a.y + (((long)b * a.OH + k) * a.OW + gj) * a.ldy + CCH * w + 16 * n + 4 * q16) =
+                    (u32x2){pack_bf16(o[0], o[1]), pack_bf16(o[2], o[3])};
+              }
+            }
+          }
+        }
+      }
+      stamp(it, 1);
+    }
+  }
+}
+
 // (C0, C1, PC, NFW, PT, RELU1, DWM, OCC = workgroups per CU) per id: 0 = block2 (147x147x64 -> 74x74x128), 1 = block3
 // (74x74x128 -> 37x37x256, the asymmetric 74 -> 37 pool: leading pad 0); 100 + id: the same
 // with per-phase s_memtime stamps (EntryBlockArgs.stamps; diagnostics only); 2, 3: 0, 1 with the
@@ -579,6 +944,15 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
 // with 13-column strips, small enough (LDS, <= 128 VGPRs) for two workgroups per CU. Measured and removed (round 5,
 // profiles/entry_block3_r5.txt): block3 as 16 waves of one slice (VALU / MFMA depthwise: 328 / 246 us)
 // and block3 with the MFMA depthwise (378 us) against config 1's 188 us -- all spill (78 / 56 / 91 VGPRs)
+// 13 / 113: block2 warp-specialized (entry_block_ws_kernel, 16 waves: 8 producers run the depthwise of
+// later steps while 8 consumers run the GEMMs of earlier ones; 13-column strips), plain / stamped.
+// 210.5 us against config 2's 216.2 / config 5's 208.4 (profiles/entry_block_ab_r4.txt, round 5): the
+// producers' LDS-latency-bound depthwise (6,336 cycles per step) stays the critical path, consumers idle
+// 37 %. The 8-wave build (4 + 4) ran 280.4 us (producers 10,252 cycles per step) and was removed.
+#define KDL_EBW_CONFIGS(X) \
+  X(13, 64, 128, 13, 16, 1, false) \
+  X(113, 64, 128, 13, 16, 1, false)
+
 #define KDL_EB_CONFIGS(X)                          \
   X(0, 64, 128, 15, 1, 1, false, false, 1)         \
   X(1, 128, 256, 13, 2, 0, true, false, 1)         \
@@ -597,6 +971,10 @@ int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds, int* occ) {
   case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbGeom<c0_, c1_, pc_, nfw, dwm>::BYTES; *occ = occ_; return 0;
     KDL_EB_CONFIGS(KDL_EBINFO)
 #undef KDL_EBINFO
+#define KDL_EBWINFO(id, c0_, c1_, pc_, nw, pt, r_) \
+  case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbwGeom<c0_, c1_, pc_, nw>::BYTES; *occ = 1; return 0;
+    KDL_EBW_CONFIGS(KDL_EBWINFO)
+#undef KDL_EBWINFO
     default: return -1;
   }
 }
@@ -606,6 +984,9 @@ static int eb_pad(int cfg) {
 #define KDL_EBPAD(id, c0_, c1_, pc_, nfw, pt, r_, dwm, occ_) case id: return pt;
     KDL_EB_CONFIGS(KDL_EBPAD)
 #undef KDL_EBPAD
+#define KDL_EBWPAD(id, c0_, c1_, pc_, nw, pt, r_) case id: return pt;
+    KDL_EBW_CONFIGS(KDL_EBWPAD)
+#undef KDL_EBWPAD
     default: return -1;
   }
 }
@@ -625,6 +1006,13 @@ hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
     break;
     KDL_EB_CONFIGS(KDL_EBCASE)
 #undef KDL_EBCASE
+#define KDL_EBWCASE(id, c0_, c1_, pc_, nw, pt, r_)                                                      \
+  case id:                                                                                            \
+    hipLaunchKernelGGL((entry_block_ws_kernel<c0_, c1_, pc_, nw, pt, r_, (id >= 100)>), dim3(a.grid),  \
+                       dim3(64 * nw), 0, s, a);   /* static LDS */                                   \
+    break;
+    KDL_EBW_CONFIGS(KDL_EBWCASE)
+#undef KDL_EBWCASE
   }
   return hipGetLastError();
 }

@@ -23,7 +23,7 @@ def stamps(p, blocks, B):
         b = X.SPEC[blk - 1]
         s1, s2, r = XE._sep(p, b.main[0], "cuda"), XE._sep(p, b.main[1], "cuda"), XE._pw(p, b.res_conv, "cuda")
         H, C0 = geom[blk]
-        cfgs = [0, 2, 4, 5] if blk == 2 else [1]
+        cfgs = [0, 2, 4, 5, 13] if blk == 2 else [1]
         for cfg in [c for b in cfgs for c in (b, 100 + b)]:
             eb = EntryBlock(f"block{blk}", s1, s2, r, cfg=cfg)
             x = torch.randn(B, H, H, C0, device="cuda").to(torch.bfloat16)
@@ -45,6 +45,21 @@ def stamps(p, blocks, B):
             if cfg < 100:
                 continue
             v = st.view(8, 64, 5).cpu().tolist()
+            if cfg == 113:      # warp-specialized: [consumer start, consumer end, producer start, producer end]
+                ph = {n: [] for n in ("iteration", "consumers busy", "producers busy")}
+                for wg in range(8):
+                    for k in range(3, 62):
+                        a0, a1 = v[wg][k], v[wg][k + 1]
+                        if 0 in a0[:4] or a1[0] == 0:
+                            continue
+                        ph["iteration"].append(a1[0] - a0[0])
+                        ph["consumers busy"].append(a0[1] - a0[0])
+                        ph["producers busy"].append(a0[3] - a0[2])
+                print("  per iteration (= one step; median shader cycles, 8 workgroups):", flush=True)
+                for n, xs in ph.items():
+                    if xs:
+                        print(f"    {n:20s} {statistics.median(xs):8.0f}", flush=True)
+                continue
             ph = {n: [] for n in ("P1 dw1", "P2 gemm1", "P3 dw2", "P4 gemm2+pool", "out+B0")}
             steps_ = 0
             for wg in range(8):
