@@ -15,6 +15,9 @@
 #include "runtime/dp_loop.h"
 #include "runtime/dp_schedule.h"
 #include "runtime/executor.h"
+#include "runtime/grpc_front.h"
+#include "runtime/grpc_load.h"
+#include "runtime/h2.h"
 #include "runtime/sstable.h"
 #include "runtime/tfproto.h"
 
@@ -32,29 +35,17 @@ py::dict spec_dict(const ModelSpecView& s) {
   return d;
 }
 
-// f32 compat payload -> uint8 pixels when it is EXACTLY float32(u) / 127.5 - 1 for 8-bit u (what
-// the reference gateway sends: keras_image_helper's Xception preprocessing, model_server.py:18),
-// so the request rides the uint8 path (4x fewer bytes to stage, copy and decode). False (dst
-// undefined) at the first block holding a value that is not. Branch-free and vectorized (an
-// AVX2 clone picked at load time where the CPU has it): the round-4 form called std::nearbyint
-// per element and clamped with float min/max, which kept the loop scalar -- 1.2 ms per 299x299x3
-// image, more than all the rest of a request's server time (profiles/serve_f32_exact_r5.txt).
-__attribute__((target_clones("avx2", "default"))) bool f32_to_u8_exact(const float* __restrict x,
-                                                                       uint8_t* __restrict u, size_t n) {
-  const size_t B = 4096;                 // blocks: early exit between them
-  for (size_t i0 = 0; i0 < n; i0 += B) {
-    const size_t i1 = std::min(n, i0 + B);
-    int bad = 0;
-    for (size_t i = i0; i < i1; ++i) {
-      int r = (int)((x[i] + 1.0f) * 127.5f + 0.5f);   // NaN / out of range -> INT_MIN: clamped, then mismatches
-      r = r < 0 ? 0 : r > 255 ? 255 : r;
-      bad |= (float)r / 127.5f - 1.0f != x[i];       // rebuilt exactly as the gateway computed it
-      u[i] = (uint8_t)r;
+// the GIL must be free while the front joins its threads (slow-path threads take it), and
+// held while its Python slow-path callable is released
+struct FrontDeleter {
+  void operator()(GrpcFront* f) const {
+    {
+      py::gil_scoped_release nogil;
+      f->stop();
     }
-    if (bad) return false;
+    delete f;
   }
-  return true;
-}
+};
 
 }  // namespace
 
@@ -177,7 +168,8 @@ PYBIND11_MODULE(_rt, m) {
       })
       .def_readonly("oldest_enqueue_us", &Batch::oldest_enqueue_us);
 
-  py::class_<DynamicBatcher>(m, "DynamicBatcher")
+  // shared holder: the native gRPC front-end's routes keep a signature's batcher alive
+  py::class_<DynamicBatcher, std::shared_ptr<DynamicBatcher>>(m, "DynamicBatcher")
       .def(py::init([](int max_batch_size, int64_t batch_timeout_us, int max_enqueued_batches,
                        std::vector<int> allowed_batch_sizes, size_t item_bytes, int out_cols, int copy_threads) {
              BatcherOptions o;
@@ -188,7 +180,7 @@ PYBIND11_MODULE(_rt, m) {
              o.allowed_batch_sizes = allowed_batch_sizes;
              o.item_bytes = item_bytes;
              o.out_cols = out_cols;
-             return new DynamicBatcher(o);
+             return std::make_shared<DynamicBatcher>(o);
            }),
            py::arg("max_batch_size") = 32, py::arg("batch_timeout_us") = 2000,
            py::arg("max_enqueued_batches") = 1000, py::arg("allowed_batch_sizes") = std::vector<int>{},
@@ -238,6 +230,83 @@ PYBIND11_MODULE(_rt, m) {
         d["padded_items"] = s.padded_items; d["queue_items"] = s.queue_items;
         return d;
       });
+  // ---- native gRPC front-end (runtime/grpc_front.h) + the native load generator
+  py::class_<GrpcFront, std::unique_ptr<GrpcFront, FrontDeleter>>(m, "GrpcFront")
+      // slow(path: str, message: bytes, deadline_us: int) -> (code, message, body: bytes, [(k, v)])
+      .def(py::init([](const std::string& host, int port, int io_threads, int slow_threads, py::function slow) {
+             auto fn = std::make_shared<py::function>(std::move(slow));
+             SlowFn cb = [fn](const std::string& path, const std::string& msg, int64_t deadline_us) {
+               py::gil_scoped_acquire gil;
+               SlowReply r;
+               py::tuple t = (*fn)(path, py::bytes(msg), deadline_us);
+               r.code = t[0].cast<int>();
+               r.message = t[1].cast<std::string>();
+               r.body = t[2].cast<std::string>();
+               for (auto kv : t[3].cast<py::list>()) {
+                 auto p = kv.cast<py::tuple>();
+                 r.meta.emplace_back(p[0].cast<std::string>(), p[1].cast<std::string>());
+               }
+               return r;
+             };
+             // built with the GIL held: a constructor that throws drops the callable safely (its
+             // threads never wait on Python before a request arrives)
+             return std::unique_ptr<GrpcFront, FrontDeleter>(
+                 new GrpcFront(host, port, io_threads, slow_threads, std::move(cb)));
+           }),
+           py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("slow_threads") = 4, py::arg("slow"))
+      .def_property_readonly("port", &GrpcFront::port)
+      .def("set_route", [](GrpcFront& f, const std::string& model, const std::string& signature, int64_t version,
+                           const std::string& input_key, const std::string& output_key, int dtype, int image,
+                           int out_cols, std::shared_ptr<DynamicBatcher> batcher, std::shared_ptr<DynamicBatcher> u8) {
+             FrontRoute r;
+             r.model = model; r.signature = signature; r.version = version; r.input_key = input_key;
+             r.output_key = output_key; r.dtype = dtype; r.image = image; r.out_cols = out_cols;
+             r.batcher = std::move(batcher); r.u8 = std::move(u8);
+             f.set_route(std::move(r));
+           },
+           py::arg("model"), py::arg("signature"), py::arg("version"), py::arg("input_key"), py::arg("output_key"),
+           py::arg("dtype"), py::arg("image"), py::arg("out_cols"), py::arg("batcher"), py::arg("u8") = nullptr)
+      .def("clear_routes", &GrpcFront::clear_routes)
+      .def("stop", &GrpcFront::stop, py::call_guard<py::gil_scoped_release>())
+      .def("stats", [](const GrpcFront& f) {
+        const FrontStats s = f.stats();
+        py::dict d;
+        d["fast_ok"] = s.fast_ok; d["fast_err"] = s.fast_err; d["slow"] = s.slow; d["exact_u8"] = s.exact_u8;
+        d["connections"] = s.connections; d["open_connections"] = s.open_connections;
+        py::dict codes;
+        for (int i = 0; i < 17; ++i)
+          if (s.by_code[i]) codes[py::int_(i)] = s.by_code[i];
+        d["by_code"] = codes;
+        py::list lat;
+        for (int i = 0; i <= kFrontLatBuckets; ++i) lat.append(s.lat[i]);
+        d["lat_counts"] = lat;
+        d["lat_sum_ms"] = s.lat_sum_ms;
+        return d;
+      });
+  m.def("grpc_percent_encode", &grpc_percent_encode);
+  m.def("http2_available", [] {
+    std::string why;
+    const bool ok = h2::api(&why) != nullptr;
+    return py::make_tuple(ok, why);
+  });
+  m.def("grpc_load", [](const std::string& host, int port, const std::string& path, py::bytes message, int conns,
+                        int streams, double seconds, double warm_s, double timeout_s) {
+          std::string msg = message;
+          LoadResult r;
+          {
+            py::gil_scoped_release nogil;
+            r = grpc_load(host, port, path, msg, conns, streams, seconds, warm_s, timeout_s);
+          }
+          py::dict d;
+          d["ok"] = r.ok; d["failed"] = r.failed; d["seconds"] = r.seconds; d["error"] = r.error;
+          d["lat_ms"] = r.lat_ms;
+          py::dict codes;
+          for (auto& kv : r.codes) codes[py::int_(kv.first)] = kv.second;
+          d["codes"] = codes;
+          return d;
+        }, py::arg("host"), py::arg("port"), py::arg("path"), py::arg("message"), py::arg("conns") = 4,
+        py::arg("streams") = 8, py::arg("seconds") = 5.0, py::arg("warm_s") = 1.0, py::arg("timeout_s") = 30.0);
+
   // ---- native batch executor (executor.h) + the fake device backend used by CPU tests
   py::class_<ExecGroup>(m, "ExecGroup")
       .def(py::init<>())

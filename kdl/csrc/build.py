@@ -45,7 +45,8 @@ GPU_SOURCES = sorted((HERE / "kernels").glob("*.hip")) + [HERE / "runtime" / "en
                                                          HERE / "runtime" / "hip_backend.cpp",
                                                          HERE / "runtime" / "comm.cpp",
                                                          HERE / "bindings_gpu.cpp"]
-RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp")] + [
+RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp",
+                                                "h2.cpp", "grpc_front.cpp", "grpc_load.cpp")] + [
     HERE / "bindings_rt.cpp"]
 HEADERS = sorted(HERE.rglob("*.h"))
 
@@ -118,7 +119,8 @@ def build_rt(force: bool = False, njobs: int = 8, verbose: bool = True) -> Path:
     _compile_all(jobs, njobs)
     if force or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         tmp = out.with_name(out.name + ".tmp")
-        _run([cxx, "-shared", "-fPIC", "-pthread", *map(str, objs), "-o", str(tmp)])
+        # libnghttp2 (the native gRPC front-end's HTTP/2) is dlopen'ed at first use (runtime/h2.cpp)
+        _run([cxx, "-shared", "-fPIC", "-pthread", *map(str, objs), "-ldl", "-o", str(tmp)])
         os.replace(tmp, out)
         if verbose:
             print(f"[kdl.build] linked {out.relative_to(ROOT)}", flush=True)

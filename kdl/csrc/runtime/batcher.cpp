@@ -88,8 +88,19 @@ int DynamicBatcher::bucket_for(int n) const {
 }
 
 int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadline_us, bool device) {
-  if (n_items <= 0 || n_items > opt_.max_batch_size) return -ST_ERROR;
   std::lock_guard<std::mutex> lk(mu_);
+  return enqueue_locked(data, n_items, deadline_us, device, nullptr);
+}
+
+int64_t DynamicBatcher::submit_async(const uint8_t* data, int n_items, int64_t deadline_us, DoneFn done) {
+  if (!done) return -ST_ERROR;
+  std::lock_guard<std::mutex> lk(mu_);
+  return enqueue_locked(data, n_items, deadline_us, false, std::move(done));
+}
+
+int64_t DynamicBatcher::enqueue_locked(const uint8_t* data, int n_items, int64_t deadline_us, bool device,
+                                       DoneFn done) {
+  if (n_items <= 0 || n_items > opt_.max_batch_size) return -ST_ERROR;
   if (shutdown_) return -ST_SHUTDOWN;
   if (queued_items_ + n_items > int64_t(opt_.max_enqueued_batches) * opt_.max_batch_size) {
     ++st_.rejected;
@@ -102,8 +113,9 @@ int64_t DynamicBatcher::submit(const uint8_t* data, int n_items, int64_t deadlin
   r->n_items = n_items;
   r->enqueue_us = now_us();
   r->deadline_us = deadline_us;
+  r->done = std::move(done);
   queue_.push_back(r);
-  live_[r->ticket] = r;
+  (r->done ? async_live_ : live_)[r->ticket] = r;   // async requests are never wait()ed
   queued_items_ += n_items;
   ++st_.submitted;
   cv_consumer_.notify_one();
@@ -154,7 +166,11 @@ int DynamicBatcher::wait(int64_t ticket, float* out, size_t out_floats) {
 }
 
 bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, bool eager) {
-  std::vector<std::shared_ptr<Req>> take;
+  std::vector<std::shared_ptr<Req>> take, expired;
+  struct Fire {                              // async callbacks of expired requests, outside the lock
+    std::vector<std::shared_ptr<Req>>& v;
+    ~Fire() { for (auto& r : v) r->done(ST_DEADLINE, nullptr, 0); }
+  } fire{expired};
   {
     std::unique_lock<std::mutex> lk(mu_);
     const int64_t give_up = now_us() + poll_us;
@@ -168,6 +184,10 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
           (*q)->status = ST_DEADLINE;
           queued_items_ -= (*q)->n_items;
           ++st_.expired;
+          if ((*q)->done) {
+            async_live_.erase((*q)->ticket);
+            expired.push_back(*q);
+          }
           q = queue_.erase(q);
           cv_producer_.notify_all();
         } else {
@@ -242,10 +262,21 @@ bool DynamicBatcher::next_batch(uint8_t* staging, int64_t poll_us, Batch* b, boo
 }
 
 void DynamicBatcher::finish(const Batch& b, const float* results, int status) {
+  std::vector<std::pair<std::shared_ptr<Req>, size_t>> async;   // (request, its batch index)
+  {
   std::lock_guard<std::mutex> lk(mu_);
   for (size_t i = 0; i < b.tickets.size(); ++i) {
     auto it = live_.find(b.tickets[i]);
-    if (it == live_.end()) continue;
+    if (it == live_.end()) {
+      auto a = async_live_.find(b.tickets[i]);
+      if (a != async_live_.end()) {
+        a->second->state = DONE;
+        ++st_.completed;
+        async.emplace_back(std::move(a->second), i);
+        async_live_.erase(a);
+      }
+      continue;
+    }
     auto& r = it->second;
     if (r->state == ABANDONED) continue;
     r->status = status;
@@ -258,13 +289,35 @@ void DynamicBatcher::finish(const Batch& b, const float* results, int status) {
     ++st_.completed;
   }
   cv_producer_.notify_all();
+  }
+  for (auto& [r, i] : async) {
+    const bool rows = status == ST_OK && results;
+    r->done(rows ? status : (status == ST_OK ? ST_ERROR : status),
+            rows ? results + size_t(b.first_item[i]) * opt_.out_cols : nullptr,
+            rows ? size_t(b.n_items[i]) * opt_.out_cols : 0);
+  }
 }
 
 void DynamicBatcher::shutdown() {
-  std::lock_guard<std::mutex> lk(mu_);
-  shutdown_ = true;
-  cv_consumer_.notify_all();
-  cv_producer_.notify_all();
+  std::vector<std::shared_ptr<Req>> dropped;   // queued async requests: answered here
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    shutdown_ = true;
+    for (auto q = queue_.begin(); q != queue_.end();) {
+      if ((*q)->done) {
+        (*q)->state = ABANDONED;
+        queued_items_ -= (*q)->n_items;
+        async_live_.erase((*q)->ticket);
+        dropped.push_back(*q);
+        q = queue_.erase(q);
+      } else {
+        ++q;
+      }
+    }
+    cv_consumer_.notify_all();
+    cv_producer_.notify_all();
+  }
+  for (auto& r : dropped) r->done(ST_SHUTDOWN, nullptr, 0);
 }
 
 BatcherStats DynamicBatcher::stats() const {

@@ -19,6 +19,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -99,6 +100,13 @@ class DynamicBatcher {
   // until the batch's device work is done, not only until wait() (deadline-expired tickets
   // return early), so device payloads come from buffers that are recycled, never freed.
   int64_t submit(const uint8_t* data, int n_items, int64_t deadline_us, bool device = false);
+  // Callback form for event-driven producers (the native gRPC front-end, runtime/grpc_front.h):
+  // nothing blocks; `done(status, rows, n_floats)` runs exactly once -- on the executor thread
+  // that finishes the batch (rows valid only during the call), on the consumer that drops the
+  // expired request, or in shutdown() -- never under the batcher's lock. `data` must stay valid
+  // until then. Returns the ticket, or -status without calling `done`.
+  using DoneFn = std::function<void(int status, const float* rows, size_t n_floats)>;
+  int64_t submit_async(const uint8_t* data, int n_items, int64_t deadline_us, DoneFn done);
   // Blocks until the request completes or its deadline passes; copies
   // n_items*out_cols floats into `out`, which holds `out_floats` floats (a smaller
   // buffer is not written and the call returns ST_ERROR). Returns a BatchStatus.
@@ -127,12 +135,15 @@ class DynamicBatcher {
     State state = QUEUED;
     int status = ST_PENDING;
     std::vector<float> result;
+    DoneFn done;                             // submit_async: completion callback (no wait())
   };
+  int64_t enqueue_locked(const uint8_t* data, int n_items, int64_t deadline_us, bool device, DoneFn done);
   BatcherOptions opt_;
   mutable std::mutex mu_;
   std::condition_variable cv_consumer_, cv_producer_;
   std::deque<std::shared_ptr<Req>> queue_;
   std::unordered_map<int64_t, std::shared_ptr<Req>> live_;
+  std::unordered_map<int64_t, std::shared_ptr<Req>> async_live_;   // submit_async tickets until done
   int64_t next_ticket_ = 1, next_batch_ = 1, queued_items_ = 0;
   bool shutdown_ = false;
   BatcherStats st_;

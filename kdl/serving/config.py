@@ -56,6 +56,10 @@ class ServerConfig:
     batching: BatchingParams = field(default_factory=BatchingParams)
     file_system_poll_wait_seconds: int = 1
     grpc_max_threads: int = 64
+    # native: the C++ gRPC front-end (runtime/grpc_front.h; Predict fast path without Python);
+    # python: the grpcio server. Falls back to python when libnghttp2 is missing
+    grpc_frontend: str = "native"
+    grpc_io_threads: int = 4      # native front-end epoll workers (one SO_REUSEPORT listener each)
     rest_api_num_threads: int = 16
     device: str = "auto"          # auto | cpu | gpu | null (front-end ceiling: zero-latency fake device)
     gpus: int = 0                 # 0 = all visible
@@ -115,6 +119,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--file_system_poll_wait_seconds", type=int, default=1)
     ap.add_argument("--grpc_max_threads", type=int, default=64)
     ap.add_argument("--rest_api_num_threads", type=int, default=16)
+    ap.add_argument("--grpc_frontend", choices=["native", "python"], default=None,
+                    help="native: C++ HTTP/2 front-end whose Predict fast path parses, batches and answers "
+                         "without Python; python: the grpcio server (env KDL_GRPC_FRONTEND, default native)")
+    ap.add_argument("--grpc_io_threads", type=int, default=None,
+                    help="native front-end I/O threads (env KDL_GRPC_IO_THREADS, default 4)")
     ap.add_argument("--device", choices=["auto", "cpu", "gpu", "null"], default="auto",
                     help="null: the native executor over a zero-latency fake device (logits = first "
                          "input byte + class index) -- measures the serving front-end's own ceiling")
@@ -193,6 +202,9 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         enable_batching=_truthy(a.enable_batching), batching=bp,
                         file_system_poll_wait_seconds=a.file_system_poll_wait_seconds,
                         grpc_max_threads=a.grpc_max_threads, rest_api_num_threads=a.rest_api_num_threads,
+                        grpc_frontend=a.grpc_frontend or env.get("KDL_GRPC_FRONTEND", "native"),
+                        grpc_io_threads=(a.grpc_io_threads if a.grpc_io_threads is not None
+                                         else int(env.get("KDL_GRPC_IO_THREADS", "4"))),
                         device=a.device, gpus=a.gpus, executors_per_gpu=a.executors_per_gpu,
                         synthetic=a.synthetic_model or _truthy(env.get("KDL_SYNTHETIC_MODEL", "0")),
                         labels=labels, host=a.host, dtype=a.dtype, graph=a.graph == "on",

@@ -31,10 +31,25 @@ class Histogram:
             self.samples.append(v)
 
     def quantile(self, q: float) -> float:
+        if self.n and len(self.samples) < min(self.n, 100_000):
+            # counts merged from native histograms (merge) carry no samples: the upper bound of
+            # the bucket holding the q-th observation
+            acc, want = 0, q * self.n
+            for b, c in zip(self.buckets + [float("inf")], self.counts):
+                acc += c
+                if acc >= want and c:
+                    return float(b)
         if not self.samples:
             return 0.0
         s = sorted(self.samples)
         return s[min(len(s) - 1, int(q * len(s)))]
+
+    def merge(self, counts, total: float) -> None:
+        """Add a native histogram's per-bucket counts (same buckets, +Inf last) and sum."""
+        for i, c in enumerate(counts):
+            self.counts[i] += c
+        self.n += sum(counts)
+        self.sum += total
 
 
 class Metrics:
@@ -44,6 +59,7 @@ class Metrics:
         self.hists: dict[tuple, Histogram] = {}
         self.gauges: dict[tuple, callable] = {}
         self.collectors: dict[str, callable] = {}     # key -> fn() -> list of exposition lines
+        self.pollers: dict[str, callable] = {}        # key -> fn(): folds native counters in (inc / merge_hist)
 
     def inc(self, name: str, value: float = 1.0, **labels) -> None:
         with self._lock:
@@ -56,6 +72,28 @@ class Metrics:
             if h is None:
                 h = self.hists[key] = Histogram(buckets)
             h.observe(value)
+
+    def merge_hist(self, name: str, counts, total: float, buckets=LAT_BUCKETS_MS, **labels) -> None:
+        key = (name, tuple(sorted(labels.items())))
+        with self._lock:
+            h = self.hists.get(key)
+            if h is None:
+                h = self.hists[key] = Histogram(buckets)
+            h.merge(counts, total)
+
+    def poller(self, key: str, fn) -> None:
+        """Register fn(), run before every render / snapshot (native front-end counters)."""
+        self.pollers[key] = fn
+
+    def drop_poller(self, key: str) -> None:
+        self.pollers.pop(key, None)
+
+    def _poll(self) -> None:
+        for fn in list(self.pollers.values()):
+            try:
+                fn()
+            except Exception:  # noqa: BLE001 - a broken poller must not break scraping
+                pass
 
     def gauge(self, name: str, fn, **labels) -> None:
         self.gauges[(name, tuple(sorted(labels.items())))] = fn
@@ -78,6 +116,7 @@ class Metrics:
         return "{" + ",".join(f'{k}="{v}"' for k, v in items) + "}"
 
     def render(self) -> str:
+        self._poll()
         out = []
         with self._lock:
             for (name, labels), v in sorted(self.counters.items()):
@@ -109,6 +148,7 @@ class Metrics:
         window, like a scrape does."""
         def key(name, labels):
             return name + ("{" + ",".join(f"{k}={v}" for k, v in labels) + "}" if labels else "")
+        self._poll()
         out: dict = {"counters": {}, "histograms": {}, "gauges": {}}
         with self._lock:
             for (name, labels), v in sorted(self.counters.items()):

@@ -51,6 +51,9 @@ class ModelManager:
         self.states: dict[int, tuple[int, str]] = {}   # version -> (state, error message)
         self._stop = threading.Event()
         self._poller: threading.Thread | None = None
+        # called (no arguments) whenever the set of live versions changes: the native gRPC
+        # front-end drops its cached routes (serving/native_front.py)
+        self.listeners: list = []
 
     # ------------------------------------------------------------ loading
     def load_initial(self) -> None:
@@ -81,6 +84,7 @@ class ModelManager:
             self.servables[v] = s
             self.states[v] = (AVAILABLE, "")
             old = [k for k in self.servables if k != v]
+        self._changed()
         log.info("loaded %s version %d (%s) on %s in %.1fs", self.name, v, src.origin,
                  f"gpus {self.devices}" if self.devices else "cpu", time.perf_counter() - t0)
         for k in old:  # latest policy: retire older versions once the new one is live
@@ -90,10 +94,18 @@ class ModelManager:
         with self._lock:
             s = self.servables.pop(v, None)
             self.states[v] = (UNLOADING, "")
+        self._changed()
         if s is not None:
             s.close()
         with self._lock:
             self.states[v] = (END, "")
+
+    def _changed(self) -> None:
+        for fn in list(self.listeners):
+            try:
+                fn()
+            except Exception:  # noqa: BLE001 - a listener must not break loading
+                log.exception("model-change listener failed")
 
     def reload(self) -> None:
         versions = list_versions(self.base)

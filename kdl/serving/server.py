@@ -15,7 +15,7 @@ import threading
 import time
 
 from .config import ServerConfig, config_from_args
-from .grpc_server import build_grpc_server
+from .grpc_server import Servicer, build_grpc_server
 from .logs import StatsLogger, setup_logging
 from .model_repo import ModelManager
 from .rest import start_rest_server
@@ -28,6 +28,7 @@ class ModelServer:
         self.cfg = cfg
         self.manager = ModelManager(cfg)
         self.grpc = None
+        self.native = None                   # native gRPC front-end (serving/native_front.py)
         self.rest = None
         self.grpc_port = None
         self.rest_port = None
@@ -36,9 +37,21 @@ class ModelServer:
         cfg = self.cfg
         # serve health/status immediately; Predict returns UNAVAILABLE until loaded
         reuse = cfg.gpu_index >= 0           # a child of the --procs launcher: ports are shared
-        self.grpc, self.grpc_port, _ = build_grpc_server(self.manager, cfg.host, cfg.port, cfg.grpc_max_threads,
-                                                         reuse_port=reuse, f32_exact_u8=cfg.f32_exact_u8)
-        self.grpc.start()
+        if cfg.grpc_frontend == "native":
+            from . import native_front
+            ok, why = native_front.available()
+            if ok:
+                self.native = native_front.NativeFront(self.manager, Servicer(self.manager, cfg.f32_exact_u8),
+                                                       cfg.host, cfg.port, io_threads=cfg.grpc_io_threads,
+                                                       slow_threads=cfg.grpc_max_threads,
+                                                       f32_exact_u8=cfg.f32_exact_u8)
+                self.grpc_port = self.native.port
+            else:
+                log.warning("native gRPC front-end unavailable (%s): serving gRPC with grpcio", why)
+        if self.native is None:
+            self.grpc, self.grpc_port, _ = build_grpc_server(self.manager, cfg.host, cfg.port, cfg.grpc_max_threads,
+                                                             reuse_port=reuse, f32_exact_u8=cfg.f32_exact_u8)
+            self.grpc.start()
         if cfg.rest_api_port:
             self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port, reuse_port=reuse,
                                           f32_exact_u8=cfg.f32_exact_u8)
@@ -59,6 +72,8 @@ class ModelServer:
         return self
 
     def stop(self, grace: float = 2.0) -> None:
+        if self.native:
+            self.native.stop()
         if self.grpc:
             self.grpc.stop(grace)
         if self.rest:

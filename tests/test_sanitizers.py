@@ -11,7 +11,8 @@ import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "kdl" / "csrc"
-RT = [CSRC / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp")]
+RT = [CSRC / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp",
+                                     "h2.cpp", "grpc_front.cpp", "grpc_load.cpp")]
 
 pytestmark = pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 # TSAN: LLVM's runtime. GCC 11's libtsan does not intercept pthread_cond_clockwait (what
@@ -24,7 +25,7 @@ CLANG = next((c for c in ("/opt/rocm/lib/llvm/bin/clang++", shutil.which("clang+
 def _build(tmp_path, name, main, flags, cxx="g++"):
     exe = tmp_path / name
     cmd = [cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, str(main),
-           *[str(s) for s in RT], "-I", str(CSRC), "-o", str(exe), "-lpthread"]
+           *[str(s) for s in RT], "-I", str(CSRC), "-o", str(exe), "-lpthread", "-ldl"]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     return exe
 
@@ -86,6 +87,23 @@ def test_dp_loopback_under_asan_ubsan(tmp_path):
     exe = _build(tmp_path, "dp_asan", CSRC / "tests" / "dp_loop_stress.cpp",
                  ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
     r = _run(exe, 4, 3, 25, env={"ASAN_OPTIONS": "detect_leaks=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(CLANG is None, reason="needs clang++ (LLVM TSAN runtime)")
+def test_native_grpc_front_under_tsan(tmp_path):
+    """The native gRPC front-end (grpc_front.h): epoll workers + slow pool + eventfd mailbox +
+    batcher callbacks under fast- and slow-path load, routes flipping, stop with calls in flight."""
+    exe = _build(tmp_path, "front_tsan", CSRC / "tests" / "front_stress.cpp", ["-fsanitize=thread"], cxx=CLANG)
+    r = _run(exe, 4, 4, 2, env={"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr
+
+
+def test_native_grpc_front_under_asan_ubsan(tmp_path):
+    exe = _build(tmp_path, "front_asan", CSRC / "tests" / "front_stress.cpp",
+                 ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
+    r = _run(exe, 4, 4, 2, env={"ASAN_OPTIONS": "detect_leaks=1"})
     assert r.returncode == 0, r.stdout + r.stderr
 
 

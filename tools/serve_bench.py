@@ -5,6 +5,11 @@ reports throughput (images/s) and p50/p99 request latency. Starts an in-process
 server on a synthetic model unless --target is given.
 
   python tools/serve_bench.py --clients 64 --images 1 --seconds 20 --signature serving_uint8
+  python tools/serve_bench.py --client native --conns 8 --clients 64 --device null   # front-end ceiling
+
+--client native drives the server with the C++ load generator (kdl._rt.grpc_load: HTTP/2
+connections each keeping clients/conns calls in flight); Python clients top out near 1-2k
+req/s per process at one image per request, below what the native front-end serves.
 """
 from __future__ import annotations
 
@@ -69,6 +74,7 @@ def _launch_procs(a):
            f"--warm_signatures={a.signature}"]
     if a.executors_per_gpu:
         cmd.append(f"--executors_per_gpu={a.executors_per_gpu}")
+    cmd.append(f"--grpc_frontend={a.frontend}")
     p = subprocess.Popen(cmd, cwd=root, env=dict(os.environ, PYTHONPATH=root), stdout=subprocess.DEVNULL,
                          stderr=subprocess.DEVNULL, start_new_session=True)
     target = f"127.0.0.1:{port}"
@@ -119,6 +125,12 @@ def main(argv=None) -> int:
                     help="in-process server: f32 requests that are exact 8-bit pixels are NOT moved to the uint8 path")
     ap.add_argument("--stages", action="store_true",
                     help="in-process server: print the native executor's mean per-stage times")
+    ap.add_argument("--frontend", choices=["native", "python"], default="native",
+                    help="server gRPC front-end: native (C++ HTTP/2, Predict fast path) or python (grpcio)")
+    ap.add_argument("--client", choices=["python", "native"], default="python",
+                    help="native: the C++ closed-loop load generator (--conns connections, clients/conns "
+                         "calls in flight on each)")
+    ap.add_argument("--conns", type=int, default=8, help="--client native: HTTP/2 connections")
     ap.add_argument("--client-procs", type=int, default=0,
                     help="run the clients in this many spawned processes (0: threads of the server "
                          "process, which then share its GIL with the server's handlers)")
@@ -127,7 +139,7 @@ def main(argv=None) -> int:
     H, W = (299, 299) if a.signature != "serving_image" else map(int, a.image_size.split("x"))
     u8 = rng.integers(0, 256, (a.images, H, W, 3), dtype=np.uint8)
     procs = []
-    if a.client_procs:
+    if a.client_procs and a.client == "python":
         import multiprocessing as mp
         from kdl.gateway.client import make_request as _mk
         if a.signature != "serving_default":
@@ -161,7 +173,7 @@ def main(argv=None) -> int:
         cfg = ServerConfig(port=0, rest_api_port=0, model_base_path=base, device=a.device, gpus=a.gpus,
                            executors_per_gpu=a.executors_per_gpu,
                            host="127.0.0.1", file_system_poll_wait_seconds=0, grpc_max_threads=max(64, a.clients * 2),
-                           f32_exact_u8=not a.no_f32_exact,
+                           f32_exact_u8=not a.no_f32_exact, grpc_frontend=a.frontend,
                            batching=BatchingParams(max_batch_size=a.max_batch, batch_timeout_micros=a.timeout_us,
                                                    allowed_batch_sizes=sizes, eager_when_idle=not a.no_eager))
         srv = ModelServer(cfg).start(block_until_loaded=True)
@@ -173,7 +185,19 @@ def main(argv=None) -> int:
     else:
         req = make_request(u8.astype(np.float32) / 127.5 - 1).SerializeToString()
     lat, lock = [], threading.Lock()
-    stop = time.perf_counter() + a.seconds
+    native_load = None
+    if a.client == "native":
+        from kdl.ops import _lib
+        host, port = target.rsplit(":", 1)
+        warm_s = min(3.0, a.seconds / 4)
+        native_load = _lib.rt().grpc_load(host, int(port), "/tensorflow.serving.PredictionService/Predict", req,
+                                          conns=a.conns, streams=max(1, a.clients // a.conns),
+                                          seconds=a.seconds - warm_s, warm_s=warm_s)
+        if native_load["error"] or native_load["failed"]:
+            print(f"native load: {native_load['failed']} failed, codes {native_load['codes']}, "
+                  f"error {native_load['error']!r}", file=sys.stderr)
+        lat = [x * 1e-3 for x in native_load["lat_ms"]]
+    stop = time.perf_counter() + (0 if native_load is not None else a.seconds)
     warm = time.perf_counter() + min(3.0, a.seconds / 4)
     if procs:
         for _, conn in procs:
@@ -193,20 +217,24 @@ def main(argv=None) -> int:
             if t0 > warm:
                 with lock:
                     lat.append(t1 - t0)
-    ths = [threading.Thread(target=client) for _ in range(0 if procs else a.clients)]
+    ths = [threading.Thread(target=client) for _ in range(0 if procs or native_load is not None else a.clients)]
     for t in ths:
         t.start()
     for t in ths:
         t.join()
-    span = stop - warm
+    span = native_load["seconds"] if native_load is not None else stop - warm
     res = {"metric": "closed-loop gRPC serving", "device": a.device, "clients": a.clients,
-           "client_procs": a.client_procs,
+           "client": a.client, "frontend": a.frontend,
+           "client_procs": a.client_procs, **({"conns": a.conns} if native_load is not None else {}),
            "images_per_request": a.images,
            "signature": a.signature, "requests": len(lat), "images_per_s": round(len(lat) * a.images / span, 1),
            "p50_ms": round(statistics.median(lat) * 1e3, 2),
            "p99_ms": round(sorted(lat)[int(0.99 * (len(lat) - 1))] * 1e3, 2)}
     if srv is not None:
         res["f32_exact_u8"] = not a.no_f32_exact
+        if srv.native is not None:
+            ns = srv.native.stats()
+            res["native_front"] = {k: ns[k] for k in ("fast_ok", "fast_err", "slow", "exact_u8")}
         run = srv.manager.get("clothing-model").runner(a.signature)
         if a.signature == "serving_image":
             res["image_size"] = a.image_size
