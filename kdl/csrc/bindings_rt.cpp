@@ -281,6 +281,10 @@ PYBIND11_MODULE(_rt, m) {
         for (int i = 0; i <= kFrontLatBuckets; ++i) lat.append(s.lat[i]);
         d["lat_counts"] = lat;
         d["lat_sum_ms"] = s.lat_sum_ms;
+        py::list wc;
+        for (int i = 0; i < FrontStats::kMaxWorkers; ++i) wc.append(s.worker_calls[i]);
+        while (py::len(wc) && wc[py::len(wc) - 1].cast<int64_t>() == 0) wc.attr("pop")();
+        d["worker_calls"] = wc;
         return d;
       });
   m.def("grpc_percent_encode", &grpc_percent_encode);

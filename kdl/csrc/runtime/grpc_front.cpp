@@ -323,6 +323,10 @@ void GrpcFront::Impl::dispatch(Worker* w, const CallP& call) {
     const int64_t t = parse_grpc_timeout(call->timeout);
     if (t > 0 && t < int64_t(1e14)) call->deadline_us = call->t0_us + t;   // > 1e8 s: none (as grpc_server.py)
   }
+  {
+    std::lock_guard<std::mutex> lk(stmu);
+    ++st.worker_calls[std::min(w->idx, FrontStats::kMaxWorkers - 1)];
+  }
   if (call->path == kPredictPath && fast_predict(w, call)) return;
   {
     std::lock_guard<std::mutex> lk(stmu);

@@ -57,6 +57,8 @@ struct FrontStats {
   int64_t by_code[17] = {};            // fast-path answers per grpc status
   int64_t lat[kFrontLatBuckets + 1] = {};   // fast-path latency histogram (ms), +Inf last
   double lat_sum_ms = 0;
+  static constexpr int kMaxWorkers = 64;
+  int64_t worker_calls[kMaxWorkers] = {};   // requests received per I/O worker (SO_REUSEPORT spread)
 };
 
 class GrpcFront {
