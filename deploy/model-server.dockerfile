@@ -11,6 +11,9 @@ ENV PYTHONUNBUFFERED=TRUE \
     MODEL_NAME=clothing-model \
     MODEL_BASE_PATH=/models
 
+# libnghttp2: HTTP/2 of the native gRPC front-end (kdl/csrc/runtime/h2.cpp dlopens it; without it
+# the server falls back to grpcio)
+RUN apt-get update && apt-get install -y --no-install-recommends libnghttp2-14 && rm -rf /var/lib/apt/lists/*
 COPY deploy/requirements-model-server.lock /tmp/requirements.lock
 RUN pip --no-cache-dir install --no-deps -r /tmp/requirements.lock
 
@@ -18,7 +21,7 @@ WORKDIR /opt/kdl
 COPY kdl ./kdl
 COPY __graft_entry__.py ./
 # compile the gfx950 HIP kernels + native executor (kdl/_C) and CPU runtime (kdl/_rt) in-tree
-RUN python -m kdl.csrc.build && python -c "import torch, kdl._C, kdl._rt"
+RUN python -m kdl.csrc.build && python -c "import torch, kdl._C, kdl._rt; assert kdl._rt.http2_available()[0]"
 
 # the SavedModel produced by tools/convert.py (or converted by `kdl convert-savedmodel`)
 COPY clothing-model /models/clothing-model/1
