@@ -121,6 +121,9 @@ struct Call {
   int64_t t0_us = 0, deadline_us = 0;
   std::vector<uint8_t> u8;               // exact-u8 copy of an f32 payload (fast path)
   bool fast = false;
+  std::shared_ptr<const FrontRoute> route;   // fast path: the route that served it
+  std::vector<float> rows;               // fast path: result rows, turned into `resp` by the worker
+  int64_t n = 0;
   int code = 0;                          // reply: grpc status, message, framed response, metadata
   std::string message, resp;
   std::vector<std::pair<std::string, std::string>> meta;
@@ -373,16 +376,15 @@ bool GrpcFront::Impl::fast_predict(Worker* w, const CallP& call) {
     }
   }
   call->fast = true;
+  call->route = r;
+  call->n = n;
   std::shared_ptr<Mailbox> mail = this->mail;
   const int64_t tk = b->submit_async(payload, int(n), call->deadline_us,
-      [call, r, mail, n](int status, const float* rows, size_t nf) {
-        if (status == ST_OK && rows && nf == size_t(n) * size_t(r->out_cols)) {
-          ModelSpecView spec;
-          spec.name = r->model;
-          spec.version = r->version;
-          spec.signature_name = r->signature;
-          const OutputTensor o{r->output_key, {n, int64_t(r->out_cols)}, rows};
-          call->resp = grpc_frame(build_predict_response({o}, spec));
+      [call, mail](int status, const float* rows, size_t nf) {
+        // runs on the executor thread that finished the batch: copy the rows only; the
+        // response is built by the connection's worker (answer), off the GPU issue path
+        if (status == ST_OK && rows && nf == size_t(call->n) * size_t(call->route->out_cols)) {
+          call->rows.assign(rows, rows + nf);
           call->code = G_OK;
         } else if (status == ST_DEADLINE) {    // serving/backend.py SignatureRunner._run's wording
           set_error(*call, G_DEADLINE, "deadline exceeded while queued for batching");
@@ -409,6 +411,15 @@ void GrpcFront::Impl::answer(Worker* w, const CallP& call) {
   Conn* c = ci->second.get();
   auto si = c->calls.find(call->stream);
   if (si == c->calls.end() || si->second != call) return;   // stream reset
+  if (call->code == G_OK && call->route && call->resp.empty()) {   // fast path: build the response here
+    const FrontRoute& r = *call->route;
+    ModelSpecView spec;
+    spec.name = r.model;
+    spec.version = r.version;
+    spec.signature_name = r.signature;
+    const OutputTensor o{r.output_key, {call->n, int64_t(r.out_cols)}, call->rows.data()};
+    call->resp = grpc_frame(build_predict_response({o}, spec));
+  }
   if (call->fast) {
     const double ms = (now_us() - call->t0_us) * 1e-3;
     std::lock_guard<std::mutex> lk(stmu);
