@@ -296,6 +296,9 @@ def main(argv=None) -> int:
             cfg.warm_signatures.append(cfg.dp_signature)
         from .model_repo import latest_version_source
         dp.share_source(latest_version_source(cfg), dev)
+        log.info("kdl model server: signature %s is served data parallel over %d GPUs (RCCL); every other "
+                 "signature runs on rank 0's GPU alone (f32 requests of exact 8-bit pixels are routed to "
+                 "the uint8 signatures by gRPC and REST alike)", cfg.dp_signature, cfg.dp_world)
     elif cfg.procs > 1:
         return launch_procs(argv, cfg)
     srv = ModelServer(cfg).start(block_until_loaded=False)
