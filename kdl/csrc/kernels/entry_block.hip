@@ -581,15 +581,15 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
 }
 
 // ===================================================================================================
-// Warp-specialized entry block (configs 12 / 112: block2). The four dependent stages of a step
-// (dw1 -> GEMM1 -> dw2 -> GEMM2 + pool) are split between two wave roles that work on DIFFERENT steps
-// at the same time, one workgroup barrier per step:
-//   producers (waves 4-7)  iteration i:  dw1(i) -> A1[i&1]   dw2(i-2) -> A2[i&1]   (MFMA depthwise)
-//                                        + the x-row DMA of step i+1, + step i's residual input row
-//   consumers (waves 0-3)  iteration i:  GEMM1(i-1) <- A1 -> y1 ring      GEMM2(i-3) <- A2 + pool
-//                                        + residual 1x1/2 GEMM + output of step i-3
-// Waves w and w+4 share a SIMD (MI355X_MICROARCH.md: cyclic wave placement), so every SIMD pairs a
-// depthwise stream with a GEMM stream instead of running the phases one after another with every wave
+// Warp-specialized entry block (configs 13 / 113: block2, NWAV = 16). The four dependent stages of a
+// step (dw1 -> GEMM1 -> dw2 -> GEMM2 + pool) are split between two wave roles that work on DIFFERENT
+// steps at the same time, one workgroup barrier per step:
+//   producers (waves NWAV/2..)  iteration i:  dw1(i) -> A1[i&1]   dw2(i-2) -> A2[i&1]   (MFMA depthwise)
+//                                             + the x-row DMA of step i+1, + step i's residual input row
+//   consumers (waves 0..NWAV/2-1) iteration i: GEMM1(i-1) <- A1 -> y1 ring   GEMM2(i-3) <- A2 + pool
+//                                             + residual 1x1/2 GEMM + output of step i-3
+// Waves w and w+4 share a SIMD (MI355X_MICROARCH.md: cyclic wave placement), so every SIMD pairs
+// depthwise streams with GEMM streams instead of running the phases one after another with every wave
 // in the same phase (the round-4 kernel: four barriers per step, ~2k cycles per phase, all of them
 // LDS-throughput bound -- profiles/entry_block_ab_r4.txt). Rings: x 8 rows (each step's DMA one
 // iteration ahead), y1 6 rows (GEMM1(i-1) writes rows R+4, R+5 of step i-2 while dw2(i-2) reads its
