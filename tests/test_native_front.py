@@ -172,9 +172,13 @@ def test_fast_path_deadline_expires_in_the_batcher(tmp_path, monkeypatch):
         assert _call(srv.grpc_port, PREDICT, req)[0] == 0          # slow path, learns the route
         batcher = srv.manager.get("clothing-model").runner("serving_uint8").batcher
         e0, f0 = batcher.stats()["expired"], srv.native.stats()["fast_ok"]
+        n0 = batcher.stats()["submitted"]
         busy = threading.Thread(target=_call, args=(srv.grpc_port, PREDICT, req))
         busy.start()
-        time.sleep(0.05)
+        t_end = time.time() + 10
+        while batcher.stats()["submitted"] == n0 and time.time() < t_end:   # the busy call holds the executor
+            time.sleep(0.005)
+        time.sleep(0.02)
         code, _, _ = _call(srv.grpc_port, PREDICT, req, timeout=0.1)
         assert code == grpc.StatusCode.DEADLINE_EXCEEDED.value[0]
         busy.join(10)
