@@ -597,14 +597,14 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
 // step i, read by consumers three iterations later). 13-column strips keep the map at 142 KiB
 // (pitch 32 px, no padding). A consumer wave owns 32 output channels of every GEMM (register-resident
 // weights); a producer wave owns a quarter of each step's depthwise units.
-template <int C0, int C1, int PC, int NWAV>
+template <int C0, int C1, int PC, int NWAV, int NCW = NWAV / 2>
 struct EbwGeom {
   static constexpr int Y2C = 2 * PC + 1, Y1C = Y2C + 2, XC = Y1C + 2;
   static constexpr int PLP = (XC + 15) / 16 * 16, PLB = PLP * 16;
   static constexpr int XROW = (C0 / 8) * PLB, Y1ROW = (C1 / 8) * PLB;
   static constexpr int KT0 = C0 / 32, KT1 = C1 / 32;
   static constexpr int Y1F = (2 * Y1C + 15) / 16, Y2FR = (Y2C + 15) / 16, Y2F = 2 * Y2FR;
-  static constexpr int NC = NWAV / 2, NP = NWAV / 2; // consumer / producer waves (w, w+4, ... share a SIMD)
+  static constexpr int NC = NCW, NP = NWAV - NCW;  // consumer / producer waves (w, w+4, ... share a SIMD)
   static constexpr int CCH = C1 / NC;                // output channels per consumer wave
   static constexpr int NSL = CCH / 16;               // 16-channel slices per consumer wave
   static constexpr int XDMA = XROW / 1024;
@@ -619,9 +619,14 @@ struct EbwGeom {
   static_assert(BYTES <= 160 * 1024, "LDS");
 };
 
-template <int C0, int C1, int PC, int NWAV, int PT, bool RELU1, bool STAMP>
+// producers store each depthwise unit as soon as it is computed (true) or after all of the step's
+// units (false: more loads in flight, more registers)
+#ifndef EBW_EAGER_STORE
+#define EBW_EAGER_STORE false
+#endif
+template <int C0, int C1, int PC, int NWAV, int NCW, int PT, bool RELU1, bool STAMP>
 __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(EntryBlockArgs a) {
-  using G = EbwGeom<C0, C1, PC, NWAV>;
+  using G = EbwGeom<C0, C1, PC, NWAV, NCW>;
   constexpr int KT0 = G::KT0, KT1 = G::KT1, PLB = G::PLB, XROW = G::XROW, Y1ROW = G::Y1ROW, XDMA = G::XDMA;
   constexpr int Y1C = G::Y1C, Y2C = G::Y2C, XC = G::XC, PLP = G::PLP;
   constexpr int Y1F = G::Y1F, Y2F = G::Y2F, Y2FR = G::Y2FR, PCOLS = G::PCOLS;
@@ -656,24 +661,6 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
     const u32x4 v = t < KT0 ? *(const u32x4*)((const uint8_t*)a.dwk1 + t * 1024 + (i % 64) * 16)
                             : *(const u32x4*)((const uint8_t*)a.dwk2 + (t - KT0) * 1024 + (i % 64) * 16);
     *(u32x4*)(s_dw + t * 1024 + (i % 64) * 16) = v;
-  }
-  // consumers: this wave's CCH output channels of every GEMM, register-resident
-  s16x8 w1[NSL][KT0], w2[NSL][KT1], wr[NSL][KT0];
-  float4 bz[3][NSL];
-  if (consumer) {
-#pragma unroll
-    for (int n = 0; n < NSL; ++n) {
-#pragma unroll
-      for (int t = 0; t < KT0; ++t) {
-        w1[n][t] = eb_frag(a.w1, NSL * w + n, KT0, t, lane);
-        wr[n][t] = eb_frag(a.wr, NSL * w + n, KT0, t, lane);
-      }
-#pragma unroll
-      for (int t = 0; t < KT1; ++t) w2[n][t] = eb_frag(a.w2, NSL * w + n, KT1, t, lane);
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-        bz[g][n] = *(const float4*)((g == 0 ? a.b1 : g == 1 ? a.b2 : a.br) + CCH * w + 16 * n + 4 * q16);
-    }
   }
   uint32_t sel[2][4];
   {
@@ -722,18 +709,19 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
     }
   };
 
-  u32x2 carry[NSL][Y2FR];                            // consumers: y2 row R+2 of the previous step
   __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));   // prologue loads landed (the waitcnt pass sees it)
   eb_lds_barrier();                                  // ring-slot bits of the step words visible
-  if (!consumer) dma_for(s0);
 
-  for (int it = s0; it < s1 + 3; ++it) {
-    // producers: step `it`'s x rows (their DMA, issued last iteration) must have landed; consumers: nothing
-    if (consumer) __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4) | (0 << 8));
-    else __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
-    eb_lds_barrier();
-    stamp(it, consumer ? 0 : 2);
-    if (!consumer) {
+  // The two roles run separate loops with the same trip count and one barrier per iteration (s_barrier
+  // counts arrivals, not program counters): each role's registers are live in its own loop only, so
+  // the consumers' register-resident weights do not sit in the producers' allocation (and the reverse)
+  if (!consumer) {
+    dma_for(s0);
+    for (int it = s0; it < s1 + 3; ++it) {
+      // step `it`'s x rows (their DMA, issued last iteration) must have landed
+      __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (0 << 8));
+      eb_lds_barrier();
+      stamp(it, 2);
       // =================================================================== producers
       const int pw = w - NC;
       if (it + 1 < s1) dma_for(it + 1);
@@ -766,7 +754,7 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
             };
             eb_dw_mfma_vals<RELU1>(tap, ent, lane, sel, dv1[i]);
             d1[i] = A1 + (t1 * Y1F + f) * 1024;
-            if constexpr (NWAV > 8) {                  // 128-VGPR builds: store at once (no deferral)
+            if constexpr (EBW_EAGER_STORE) {           // store at once (no deferral)
               eb_dw_store(d1[i], lane, dv1[i]);
               d1[i] = nullptr;
             }
@@ -802,7 +790,7 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
               };
               eb_dw_mfma_vals<false>(tap, ent, lane, sel, dv2[i]);
               d2[i] = A2 + (t2 * Y2F + f) * 1024;
-              if constexpr (NWAV > 8) {
+              if constexpr (EBW_EAGER_STORE) {
                 eb_dw_store(d2[i], lane, dv2[i]);
                 d2[i] = nullptr;
               }
@@ -817,7 +805,28 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
       for (int i = 0; i < U2W; ++i)
         if (d2[i]) eb_dw_store(d2[i], lane, dv2[i]);
       stamp(it, 3);
-    } else {
+    }
+  } else {
+    // consumers: this wave's CCH output channels of every GEMM, register-resident
+    s16x8 w1[NSL][KT0], w2[NSL][KT1], wr[NSL][KT0];
+    float4 bz[3][NSL];
+#pragma unroll
+    for (int n = 0; n < NSL; ++n) {
+#pragma unroll
+      for (int t = 0; t < KT0; ++t) {
+        w1[n][t] = eb_frag(a.w1, NSL * w + n, KT0, t, lane);
+        wr[n][t] = eb_frag(a.wr, NSL * w + n, KT0, t, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < KT1; ++t) w2[n][t] = eb_frag(a.w2, NSL * w + n, KT1, t, lane);
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+        bz[g][n] = *(const float4*)((g == 0 ? a.b1 : g == 1 ? a.b2 : a.br) + CCH * w + 16 * n + 4 * q16);
+    }
+    u32x2 carry[NSL][Y2FR];                          // y2 row R+2 of the previous step
+    for (int it = s0; it < s1 + 3; ++it) {
+      eb_lds_barrier();                              // (no VMEM to wait for: the weights' waits are the compiler's)
+      stamp(it, 0);
       // =================================================================== consumers
       if (it - 1 >= s0 && it - 1 < s1) {             // GEMM1(it - 1) <- A1[(it - 1) & 1] -> y1 ring
         int b, s, k, mode, xs;
@@ -949,9 +958,13 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
 // 210.5 us against config 2's 216.2 / config 5's 208.4 (profiles/entry_block_ab_r4.txt, round 5): the
 // producers' LDS-latency-bound depthwise (6,336 cycles per step) stays the critical path, consumers idle
 // 37 %. The 8-wave build (4 + 4) ran 280.4 us (producers 10,252 cycles per step) and was removed.
+// 14 / 114: the same with 4 consumer waves (32 channels each: every A fragment read feeds two MFMAs)
+// and 12 producer waves (the depthwise is the critical path)
 #define KDL_EBW_CONFIGS(X) \
-  X(13, 64, 128, 13, 16, 1, false) \
-  X(113, 64, 128, 13, 16, 1, false)
+  X(13, 64, 128, 13, 16, 8, 1, false) \
+  X(14, 64, 128, 13, 16, 4, 1, false) \
+  X(113, 64, 128, 13, 16, 8, 1, false) \
+  X(114, 64, 128, 13, 16, 4, 1, false)
 
 #define KDL_EB_CONFIGS(X)                          \
   X(0, 64, 128, 15, 1, 1, false, false, 1)         \
@@ -971,8 +984,8 @@ int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds, int* occ) {
   case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbGeom<c0_, c1_, pc_, nfw, dwm>::BYTES; *occ = occ_; return 0;
     KDL_EB_CONFIGS(KDL_EBINFO)
 #undef KDL_EBINFO
-#define KDL_EBWINFO(id, c0_, c1_, pc_, nw, pt, r_) \
-  case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbwGeom<c0_, c1_, pc_, nw>::BYTES; *occ = 1; return 0;
+#define KDL_EBWINFO(id, c0_, c1_, pc_, nw, nc, pt, r_) \
+  case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbwGeom<c0_, c1_, pc_, nw, nc>::BYTES; *occ = 1; return 0;
     KDL_EBW_CONFIGS(KDL_EBWINFO)
 #undef KDL_EBWINFO
     default: return -1;
@@ -984,7 +997,7 @@ static int eb_pad(int cfg) {
 #define KDL_EBPAD(id, c0_, c1_, pc_, nfw, pt, r_, dwm, occ_) case id: return pt;
     KDL_EB_CONFIGS(KDL_EBPAD)
 #undef KDL_EBPAD
-#define KDL_EBWPAD(id, c0_, c1_, pc_, nw, pt, r_) case id: return pt;
+#define KDL_EBWPAD(id, c0_, c1_, pc_, nw, nc, pt, r_) case id: return pt;
     KDL_EBW_CONFIGS(KDL_EBWPAD)
 #undef KDL_EBWPAD
     default: return -1;
@@ -1006,9 +1019,9 @@ hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
     break;
     KDL_EB_CONFIGS(KDL_EBCASE)
 #undef KDL_EBCASE
-#define KDL_EBWCASE(id, c0_, c1_, pc_, nw, pt, r_)                                                      \
+#define KDL_EBWCASE(id, c0_, c1_, pc_, nw, nc, pt, r_)                                                      \
   case id:                                                                                            \
-    hipLaunchKernelGGL((entry_block_ws_kernel<c0_, c1_, pc_, nw, pt, r_, (id >= 100)>), dim3(a.grid),  \
+    hipLaunchKernelGGL((entry_block_ws_kernel<c0_, c1_, pc_, nw, nc, pt, r_, (id >= 100)>), dim3(a.grid),  \
                        dim3(64 * nw), 0, s, a);   /* static LDS */                                   \
     break;
     KDL_EBW_CONFIGS(KDL_EBWCASE)
