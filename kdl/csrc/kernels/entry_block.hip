@@ -40,6 +40,22 @@ __device__ __attribute__((aligned(16))) uint8_t eb_zeros[256];
 
 constexpr int EB_MAX_STEPS = 128;                  // steps per workgroup (host plan checks it)
 
+// The workgroup's step words in two VGPRs: word i in lane i % 64 of v[i / 64]. A step is decoded with
+// v_readlane at its (uniform) index: no LDS round trip at the head of every step's dependency chain
+// (address math -> tap reads), which the LDS-resident table put there once per decode.
+struct EbStepRegs {
+  uint32_t v0 = 0, v1 = 0;
+  __device__ __forceinline__ void load(const uint32_t* st, int n, int lane) {
+    v0 = lane < n ? st[lane] : 0u;
+    v1 = 64 + lane < n ? st[64 + lane] : 0u;
+  }
+  __device__ __forceinline__ uint32_t get(int i) const {
+    i = __builtin_amdgcn_readfirstlane(i);
+    return (uint32_t)__builtin_amdgcn_readlane((int)(i < 64 ? v0 : v1), i & 63);
+  }
+};
+static_assert(EB_MAX_STEPS <= 128, "EbStepRegs holds two words per lane");
+
 template <int C0, int C1, int PC, int NFW, bool DWM = false>
 struct EbGeom {
   static constexpr int Y2C = 2 * PC + 1;            // y2 columns a strip needs
@@ -286,8 +302,12 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
       glds16(src, xr + (r & 3) * XROW + d * 1024);
     }
   };
+  // register-resident step words where the registers are free (1-slice, 1-workgroup-per-CU configs:
+  // block3's and the 2-workgroup configs' allocations already spill)
+  constexpr bool REG_STEPS = NFW == 1 && OCC == 1;
+  EbStepRegs str;                                     // loaded once the table is published (below)
   auto decode = [&](int q, int& b, int& s, int& k, int& mode) {
-    const uint32_t e = stl[q - s0];
+    const uint32_t e = REG_STEPS ? str.get(q - s0) : stl[q - s0];
     b = e & 255; s = (e >> 8) & 63; k = (int)((e >> 14) & 511) - 2; mode = (e >> 23) & 3;
   };
   // pooled row k pools y2 rows R..R+2, R = 2k - PT; a step computes y1 rows R+2, R+3 from x rows
@@ -321,6 +341,7 @@ __global__ __launch_bounds__(64 * (C1 / (16 * NFW)), OCC * C1 / (64 * NFW)) void
     }
   };
   __syncthreads();                                   // step table, weights, biases in LDS
+  if constexpr (REG_STEPS) str.load(stl, s1 - s0, lane);
   dma_for(s0);
   for (int q = s0; q < s1; ++q) {
     int b, s, k, mode;
@@ -684,8 +705,9 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
       s_st[i] = e | ((uint32_t)(xs & (XR - 1)) << 25);
     }
   }
+  EbStepRegs str;                                    // loaded once the ring-slot bits are in (below)
   auto decode = [&](int q, int& b, int& s, int& k, int& mode, int& xs) {
-    const uint32_t e = s_st[q - s0];
+    const uint32_t e = str.get(q - s0);
     b = e & 255; s = (e >> 8) & 63; k = (int)((e >> 14) & 511) - 2; mode = (e >> 23) & 3; xs = (e >> 25) & 7;
   };
   auto dma_for = [&](int q) {                        // producers only: step q's new x rows
@@ -711,6 +733,7 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
 
   __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));   // prologue loads landed (the waitcnt pass sees it)
   eb_lds_barrier();                                  // ring-slot bits of the step words visible
+  str.load(s_st, s1 - s0, lane);
 
   // The two roles run separate loops with the same trip count and one barrier per iteration (s_barrier
   // counts arrivals, not program counters): each role's registers are live in its own loop only, so
