@@ -645,7 +645,9 @@ struct EbwGeom {
 #ifndef EBW_EAGER_STORE
 #define EBW_EAGER_STORE false
 #endif
-template <int C0, int C1, int PC, int NWAV, int NCW, int PT, bool RELU1, bool STAMP>
+// CDW: dw2 units per step that every consumer wave computes too (the consumers idle half of an
+// iteration while the producers' depthwise is the critical path); the producers keep the rest
+template <int C0, int C1, int PC, int NWAV, int NCW, int PT, bool RELU1, bool STAMP, int CDW = 0>
 __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(EntryBlockArgs a) {
   using G = EbwGeom<C0, C1, PC, NWAV, NCW>;
   constexpr int KT0 = G::KT0, KT1 = G::KT1, PLB = G::PLB, XROW = G::XROW, Y1ROW = G::Y1ROW, XDMA = G::XDMA;
@@ -653,7 +655,9 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
   constexpr int Y1F = G::Y1F, Y2F = G::Y2F, Y2FR = G::Y2FR, PCOLS = G::PCOLS;
   constexpr int XR = G::XR, YR = G::YR, RS = G::RS, NC = G::NC, NP = G::NP, CCH = G::CCH, NSL = G::NSL;
   constexpr int U1 = KT0 * Y1F, U2 = KT1 * Y2F;
-  constexpr int U1W = (U1 + NP - 1) / NP, U2W = (U2 + NP - 1) / NP;
+  constexpr int CU2 = CDW * NC;                      // dw2 units 0..CU2-1: consumers (units w + NC j); the rest: producers
+  static_assert(CU2 % KT1 == 0 && CU2 <= U2, "consumer dw2 units keep the producers' k-step per wave");
+  constexpr int U1W = (U1 + NP - 1) / NP, U2W = (U2 - CU2 + NP - 1) / NP;
   static_assert(PT == 1, "the residual row 2k is x row R+1 of the step (odd map size: block2)");
   // distinct LDS objects: the compiler may reorder accesses of different regions
   __shared__ __attribute__((aligned(16))) uint8_t s_x[XR * XROW];
@@ -748,9 +752,9 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
       // =================================================================== producers
       const int pw = w - NC;
       if (it + 1 < s1) dma_for(it + 1);
-      u32x2 dv1[U1W][2], dv2[U2W][2];
+      u32x2 dv1[U1W][2], dv2[U2W > 0 ? U2W : 1][2];
       uint8_t* d1[U1W];
-      uint8_t* d2[U2W];
+      uint8_t* d2[U2W > 0 ? U2W : 1];
 #pragma unroll
       for (int i = 0; i < U1W; ++i) d1[i] = nullptr;
 #pragma unroll
@@ -798,7 +802,7 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
           uint8_t* const A2 = s_a2 + (it & 1) * G::A2B;
 #pragma unroll
           for (int i = 0; i < U2W; ++i) {
-            const int u = pw + NP * i;
+            const int u = CU2 + pw + NP * i;
             if (u < U2) {
               const int f = u / KT1;
               const int rr = f / Y2FR, col = (f % Y2FR) * 16 + p16;
@@ -850,6 +854,33 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
     for (int it = s0; it < s1 + 3; ++it) {
       eb_lds_barrier();                              // (no VMEM to wait for: the weights' waits are the compiler's)
       stamp(it, 0);
+      if constexpr (CDW > 0) {                       // dw2(it - 2), units w + NC j -> A2[it & 1] (read after the next barrier)
+        if (it - 2 >= s0 && it - 2 < s1) {
+          int b, s, k, mode, xs;
+          decode(it - 2, b, s, k, mode, xs);
+          if (mode >= 1) {
+            const int R = 2 * k - PT, t2 = w % KT1;
+            auto unit = [&](int u) {
+              const int f = u / KT1;
+              const int rr = f / Y2FR, col = (f % Y2FR) * 16 + p16;
+              const int row = R + 1 + rr;
+              const uint8_t* base = s_y1 + (4 * t2 + (q16 & 1)) * PLB + col * 16;
+              auto tap = [&](int g, int ti) {
+                const int yr = row - 1 + ti / 3;
+                return *(const u32x4*)(base + 2 * g * PLB + ((yr % YR + YR) % YR) * Y1ROW + (ti % 3) * 16);
+              };
+              auto ent = [&](int g) {
+                return *(const u32x4*)(s_dw + (KT0 + t2) * 1024 + (((g * 16 + p16) * 2) + (q16 >> 1)) * 16);
+              };
+              u32x2 dv[2];
+              eb_dw_mfma_vals<false>(tap, ent, lane, sel, dv);
+              eb_dw_store(s_a2 + (it & 1) * G::A2B + (t2 * Y2F + f) * 1024, lane, dv);
+            };
+            unit(w);
+            if constexpr (CDW > 1) unit(w + NC);
+          }
+        }
+      }
       // =================================================================== consumers
       if (it - 1 >= s0 && it - 1 < s1) {             // GEMM1(it - 1) <- A1[(it - 1) & 1] -> y1 ring
         int b, s, k, mode, xs;
@@ -981,13 +1012,17 @@ __global__ __launch_bounds__(64 * NWAV, NWAV / 4) void entry_block_ws_kernel(Ent
 // 210.5 us against config 2's 216.2 / config 5's 208.4 (profiles/entry_block_ab_r4.txt, round 5): the
 // producers' LDS-latency-bound depthwise (6,336 cycles per step) stays the critical path, consumers idle
 // 37 %. The 8-wave build (4 + 4) ran 280.4 us (producers 10,252 cycles per step) and was removed.
-// 14 / 114: the same with 4 consumer waves (32 channels each: every A fragment read feeds two MFMAs)
-// and 12 producer waves (the depthwise is the critical path)
+// 15 / 115 (block2's default): config 13 with every consumer wave also computing one of the step's 16
+// dw2 units (CDW = 1): 191.8 vs 199.2 us, iteration 7,212 -> 6,636 cycles (consumers busy 4,700,
+// producers 5,572), bench +1.0 % in 3 of 3 pairs. Measured and removed (profiles/entry_block_ab_r4.txt):
+// 4 consumer + 12 producer waves (227.0 us: the 32-channel consumers spill 32 VGPRs), two dw2 units per
+// consumer (215.8 us: consumers 6,168 busy with 14 VGPRs spilled), and the residual-row copy moved to the
+// consumers as well (iteration 6,732 vs 6,676, bench -0.2 %).
 #define KDL_EBW_CONFIGS(X) \
-  X(13, 64, 128, 13, 16, 8, 1, false) \
-  X(14, 64, 128, 13, 16, 4, 1, false) \
-  X(113, 64, 128, 13, 16, 8, 1, false) \
-  X(114, 64, 128, 13, 16, 4, 1, false)
+  X(13, 64, 128, 13, 16, 8, 1, false, 0) \
+  X(15, 64, 128, 13, 16, 8, 1, false, 1) \
+  X(113, 64, 128, 13, 16, 8, 1, false, 0) \
+  X(115, 64, 128, 13, 16, 8, 1, false, 1)
 
 #define KDL_EB_CONFIGS(X)                          \
   X(0, 64, 128, 15, 1, 1, false, false, 1)         \
@@ -1007,7 +1042,7 @@ int entry_block_config(int cfg, int* c0, int* c1, int* pc, int* lds, int* occ) {
   case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbGeom<c0_, c1_, pc_, nfw, dwm>::BYTES; *occ = occ_; return 0;
     KDL_EB_CONFIGS(KDL_EBINFO)
 #undef KDL_EBINFO
-#define KDL_EBWINFO(id, c0_, c1_, pc_, nw, nc, pt, r_) \
+#define KDL_EBWINFO(id, c0_, c1_, pc_, nw, nc, pt, r_, cdw) \
   case id: *c0 = c0_; *c1 = c1_; *pc = pc_; *lds = EbwGeom<c0_, c1_, pc_, nw, nc>::BYTES; *occ = 1; return 0;
     KDL_EBW_CONFIGS(KDL_EBWINFO)
 #undef KDL_EBWINFO
@@ -1020,7 +1055,7 @@ static int eb_pad(int cfg) {
 #define KDL_EBPAD(id, c0_, c1_, pc_, nfw, pt, r_, dwm, occ_) case id: return pt;
     KDL_EB_CONFIGS(KDL_EBPAD)
 #undef KDL_EBPAD
-#define KDL_EBWPAD(id, c0_, c1_, pc_, nw, nc, pt, r_) case id: return pt;
+#define KDL_EBWPAD(id, c0_, c1_, pc_, nw, nc, pt, r_, cdw) case id: return pt;
     KDL_EBW_CONFIGS(KDL_EBWPAD)
 #undef KDL_EBWPAD
     default: return -1;
@@ -1042,9 +1077,9 @@ hipError_t entry_block(int cfg, const EntryBlockArgs& a, hipStream_t s) {
     break;
     KDL_EB_CONFIGS(KDL_EBCASE)
 #undef KDL_EBCASE
-#define KDL_EBWCASE(id, c0_, c1_, pc_, nw, nc, pt, r_)                                                      \
+#define KDL_EBWCASE(id, c0_, c1_, pc_, nw, nc, pt, r_, cdw)                                                      \
   case id:                                                                                            \
-    hipLaunchKernelGGL((entry_block_ws_kernel<c0_, c1_, pc_, nw, nc, pt, r_, (id >= 100)>), dim3(a.grid),  \
+    hipLaunchKernelGGL((entry_block_ws_kernel<c0_, c1_, pc_, nw, nc, pt, r_, (id >= 100), cdw>), dim3(a.grid),  \
                        dim3(64 * nw), 0, s, a);   /* static LDS */                                   \
     break;
     KDL_EBW_CONFIGS(KDL_EBWCASE)

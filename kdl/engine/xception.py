@@ -44,11 +44,12 @@ class XceptionEngine(EngineBase):
         self.head = head
         # fused entry blocks (entry_block.hip): block numbers lowered to one launch each.
         # KDL_ENTRY_BLOCK: a list "2,3" / "2:4,3" (block[:kernel config]), "1" = blocks 2 and 3,
-        # "0" = none. Default "2:13,3": block2 on the warp-specialized kernel (producer waves run the
-        # depthwise of later rows while consumer waves run the GEMMs of earlier ones; +0.8 % over the
-        # round-4 default 2:2 in 4 of 4 interleaved pairs) and block3, whose lighter stage 1 moves the
-        # stage cut to block8_sepconv3 (profiles/entry_block_ab_r4.txt)
-        eb = os.environ.get("KDL_ENTRY_BLOCK", "2:13,3")
+        # "0" = none. Default "2:15,3": block2 on the warp-specialized kernel (producer waves run the
+        # depthwise of later rows while consumer waves run the GEMMs of earlier ones and one dw2 unit
+        # each; config 13 +0.8 % over the round-4 default 2:2 in 4 of 4 interleaved pairs, config 15
+        # +1.0 % over 13 in 3 of 3) and block3, whose lighter stage 1 moves the stage cut to
+        # block8_sepconv3 (profiles/entry_block_ab_r4.txt)
+        eb = os.environ.get("KDL_ENTRY_BLOCK", "2:15,3")
         spec = "2,3" if eb == "1" else ("" if eb == "0" else eb)
         self.fused_blocks = {}
         for v in filter(None, (x.strip() for x in spec.split(","))):

@@ -41,8 +41,8 @@ GEOM = {2: (147, 64, 74, 128), 3: (74, 128, 37, 256)}
 # lists still fit the kernel's LDS step table (EB_MAX_STEPS)
 CASES = [(2, 2, None), (2, 2, 9), (2, 3, 97), (2, 1, 8), (3, 2, None), (3, 3, 7), (3, 1, 1)]
 # kernel configs per block (entry_block.hip KDL_EB_CONFIGS): VALU / MFMA depthwise, 1 or 2 WGs per CU
-# 13 / 14: block2 warp-specialized, 16 waves, 8 / 4 consumer waves (entry_block_ws_kernel)
-BLOCK_CFGS = {2: [0, 2, 4, 5, 13, 14], 3: [1]}
+# 13 / 15: block2 warp-specialized, 16 waves (8 consumers + 8 producers; 15: the consumers also run one dw2 unit each)
+BLOCK_CFGS = {2: [0, 2, 4, 5, 13, 15], 3: [1]}
 
 
 @pytest.mark.parametrize("blk,B,grid,cfg", [c + (g,) for c in CASES for g in BLOCK_CFGS[c[0]]])
@@ -68,7 +68,7 @@ def test_entry_block_matches_oracle(xparams, blk, B, grid, cfg):
     assert err < 2e-2, err
 
 
-@pytest.mark.parametrize("B,cfg", [(96, 2), (128, 2), (128, 0), (128, 13), (128, 14)])
+@pytest.mark.parametrize("B,cfg", [(96, 2), (128, 2), (128, 0), (128, 13), (128, 15)])
 def test_entry_block2_large_bucket_runs_in_two_waves(xparams, B, cfg):
     """batch >= ~85 overflowed a one-wave plan's step table (EB_MAX_STEPS); the default
     plan now adds whole waves of workgroups. The fp32 oracle runs on the GPU at this size."""
@@ -100,7 +100,7 @@ def test_entry_block_refuses_a_step_table_over_the_lds_limit(xparams):
         eb.plan(2, 74, 74)
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 13, 14])
+@pytest.mark.parametrize("cfg", [0, 2, 13, 15])
 def test_entry_block2_replays_bit_identical(xparams, cfg):
     """Persistent kernel, host step table: two launches give identical bytes (an LDS / DMA ordering
     bug would show as run-to-run noise; VALU and MFMA depthwise configs)."""

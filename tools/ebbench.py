@@ -23,7 +23,7 @@ def stamps(p, blocks, B):
         b = X.SPEC[blk - 1]
         s1, s2, r = XE._sep(p, b.main[0], "cuda"), XE._sep(p, b.main[1], "cuda"), XE._pw(p, b.res_conv, "cuda")
         H, C0 = geom[blk]
-        cfgs = [2, 5, 13, 14] if blk == 2 else [1]
+        cfgs = [2, 13, 15] if blk == 2 else [1]
         for cfg in [c for b in cfgs for c in (b, 100 + b)]:
             eb = EntryBlock(f"block{blk}", s1, s2, r, cfg=cfg)
             x = torch.randn(B, H, H, C0, device="cuda").to(torch.bfloat16)
@@ -45,7 +45,7 @@ def stamps(p, blocks, B):
             if cfg < 100:
                 continue
             v = st.view(8, 64, 5).cpu().tolist()
-            if cfg in (113, 114):      # warp-specialized: [consumer start, consumer end, producer start, producer end]
+            if cfg in (113, 115):      # warp-specialized: [consumer start, consumer end, producer start, producer end]
                 ph = {n: [] for n in ("iteration", "consumers busy", "producers busy")}
                 for wg in range(8):
                     for k in range(3, 62):
