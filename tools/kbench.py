@@ -27,6 +27,8 @@ SHAPES = {
     "b4_sep2": (MODE_DW, 728, 728, 37, 1),
     "b14_sep2": (MODE_DW, 1536, 2048, 10, 1),
     "stem2": (MODE_CONV, 32, 64, 149, 1),
+    "b4_res": (MODE_PW, 256, 728, 37, 2),      # block4 residual 1x1/2 (conv2d_2)
+    "b13_res": (MODE_PW, 728, 1024, 19, 2),    # block13 residual 1x1/2 (conv2d_3)
     # ablations of the middle-flow GEMM: K x2 / x0.5, M x2 (via --batch)
     "mid_pw_k2": (MODE_PW, 1456, 728, 19, 1),
     "mid_pw_kh": (MODE_PW, 352, 728, 19, 1),
