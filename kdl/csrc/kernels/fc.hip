@@ -7,41 +7,68 @@
 
 namespace kdl {
 
-// one block per image, one thread per 8-channel chunk (loops if F > 2048)
+// grid (ceil(F / 8 / GAP_CG), B): a block owns GAP_CG 8-channel chunks of one image; its GAP_PARTS
+// thread groups each sum every GAP_PARTS-th pixel (four independent 16-byte loads in flight per
+// thread), then the partial sums meet in LDS. The round-1 form (one block per image, every thread
+// walking all HW pixels of its chunks in one dependent chain) ran EfficientNet-B7's 19x19x2560 pool
+// in 200 us on 32 of the 256 CUs, for 59 MB of reads (tools/layer_profile.py, round 5).
+constexpr int GAP_CG = 32, GAP_PARTS = 8;
 template <int DT>
-__global__ __launch_bounds__(256) void gap_kernel(GapArgs a) {
+__global__ __launch_bounds__(GAP_CG * GAP_PARTS) void gap_kernel(GapArgs a) {
   using E = Elt<DT>;
-  const int b = blockIdx.x;
-  const uint16_t* xb = a.x + (long)b * a.HW * a.ldx;
+  __shared__ float red[GAP_PARTS][GAP_CG][9];        // +1: no bank conflicts on the reduction reads
+  const int b = blockIdx.y, c = threadIdx.x % GAP_CG, part = threadIdx.x / GAP_CG;
+  const int F8 = a.F / 8, c8 = blockIdx.x * GAP_CG + c;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto add = [&](const u32x4 v) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      s[2 * d] += E::lo(v[d]);
+      s[2 * d + 1] += E::hi(v[d]);
+    }
+  };
+  if (c8 < F8) {
+    const uint16_t* xb = a.x + (long)b * a.HW * a.ldx + c8 * 8;
+    int p = part;
+    for (; p + 3 * GAP_PARTS < a.HW; p += 4 * GAP_PARTS) {
+      const u32x4 v0 = *(const u32x4*)(xb + (long)p * a.ldx);
+      const u32x4 v1 = *(const u32x4*)(xb + (long)(p + GAP_PARTS) * a.ldx);
+      const u32x4 v2 = *(const u32x4*)(xb + (long)(p + 2 * GAP_PARTS) * a.ldx);
+      const u32x4 v3 = *(const u32x4*)(xb + (long)(p + 3 * GAP_PARTS) * a.ldx);
+      add(v0); add(v1); add(v2); add(v3);
+    }
+    for (; p < a.HW; p += GAP_PARTS) add(*(const u32x4*)(xb + (long)p * a.ldx));
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[part][c][e] = s[e];
+  __syncthreads();
+  if (part != 0 || c8 >= F8) return;
   const float inv = 1.f / (float)a.HW;
-  for (int c8 = threadIdx.x; c8 < a.F / 8; c8 += 256) {
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int p = 0; p < a.HW; ++p) {
-      const u32x4 v = *(const u32x4*)(xb + (long)p * a.ldx + c8 * 8);
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        s[2 * d] += E::lo(v[d]);
-        s[2 * d + 1] += E::hi(v[d]);
-      }
-    }
-    if (a.y) {
-      float4* o = (float4*)(a.y + (long)b * a.F + c8 * 8);
-      o[0] = (float4){s[0] * inv, s[1] * inv, s[2] * inv, s[3] * inv};
-      o[1] = (float4){s[4] * inv, s[5] * inv, s[6] * inv, s[7] * inv};
-    }
-    if (a.yb) {
-      u32x4 o;
+  for (int e = 0; e < 8; ++e) {
+    float t = 0.f;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) o[d] = E::pack(s[2 * d] * inv, s[2 * d + 1] * inv);
-      *(u32x4*)(a.yb + (long)b * a.F + c8 * 8) = o;
-    }
+    for (int q = 0; q < GAP_PARTS; ++q) t += red[q][c][e];   // fixed order: deterministic
+    s[e] = t * inv;
+  }
+  if (a.y) {
+    float4* o = (float4*)(a.y + (long)b * a.F + c8 * 8);
+    o[0] = (float4){s[0], s[1], s[2], s[3]};
+    o[1] = (float4){s[4], s[5], s[6], s[7]};
+  }
+  if (a.yb) {
+    u32x4 o;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = E::pack(s[2 * d], s[2 * d + 1]);
+    *(u32x4*)(a.yb + (long)b * a.F + c8 * 8) = o;
   }
 }
 
 hipError_t gap(const GapArgs& a, hipStream_t s) {
-  if (a.F % 8 != 0 || a.ldx % 8 != 0 || a.B <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
-  if (a.dt) hipLaunchKernelGGL(gap_kernel<1>, dim3(a.B), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(gap_kernel<0>, dim3(a.B), dim3(256), 0, s, a);
+  if (a.F % 8 != 0 || a.ldx % 8 != 0 || a.B <= 0 || a.HW <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+  const dim3 grid((a.F / 8 + GAP_CG - 1) / GAP_CG, a.B);
+  if (a.dt) hipLaunchKernelGGL(gap_kernel<1>, grid, dim3(GAP_CG * GAP_PARTS), 0, s, a);
+  else hipLaunchKernelGGL(gap_kernel<0>, grid, dim3(GAP_CG * GAP_PARTS), 0, s, a);
   return hipGetLastError();
 }
 

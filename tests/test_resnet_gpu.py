@@ -121,6 +121,22 @@ def test_gap_fc():
     assert _rel(out2, ref2) < 1e-3
 
 
+@pytest.mark.parametrize("B,HW,Fd,ldx", [(32, 361, 2560, 2560), (3, 1, 72, 80), (5, 7, 264, 264), (2, 100, 2048, 2056)])
+def test_gap_shapes(B, HW, Fd, ldx):
+    """fc.hip gap_kernel (pixel partitions + LDS reduction) against the fp32 mean: EfficientNet-B7's
+    19x19x2560 head, fewer pixels than partitions, chunk counts that leave a block partly empty, padded rows."""
+    gen = torch.Generator().manual_seed(B * 1000 + HW)
+    x = torch.randn(B, HW, ldx, generator=gen).to(torch.bfloat16).to(DEV)
+    feat = torch.zeros(B, Fd, device=DEV)
+    fb = torch.zeros(B, Fd, dtype=torch.bfloat16, device=DEV)
+    C = _lib.lib()
+    C.gap(dict(x=x.data_ptr(), y=feat.data_ptr(), yb=fb.data_ptr(), B=B, HW=HW, ldx=ldx, F=Fd), _lib.stream_ptr())
+    torch.cuda.synchronize()
+    ref = x[:, :, :Fd].float().mean(dim=1)
+    assert _rel(feat, ref) < 1e-5
+    assert _rel(fb.float(), ref) < 1e-2
+
+
 @pytest.fixture(scope="module")
 def rparams():
     return R.init_params(seed=0)
