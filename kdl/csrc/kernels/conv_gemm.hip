@@ -291,6 +291,9 @@ static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (a.K % 32 != 0 || a.M <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+  if (cfg >= STREAM_CFG_BASE)
+    return mode == MODE_PW && cfg <= STREAM_CFG_BASE + 1 ? gemm_stream(a, cfg == STREAM_CFG_BASE + 1, s)
+                                                         : hipErrorInvalidValue;
   // split-K and per-image weights: the LDS-DMA pipelined GEMM only
   if (a.ksplit > 1 && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE)) return hipErrorInvalidValue;
   if (a.wimg && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE || a.wimg < 0)) return hipErrorInvalidValue;
@@ -315,6 +318,8 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
 }
 
 int conv_gemm_config(int cfg, int* bm, int* bn, int* threads) {
+  if (cfg == STREAM_CFG_BASE || cfg == STREAM_CFG_BASE + 1) { *bm = 16; *bn = 32; *threads = 512; return 0; }   // nominal
+  if (cfg > STREAM_CFG_BASE) return -1;
   if (cfg >= C3_CFG_BASE) return conv3x3_2d_config(cfg - C3_CFG_BASE, bm, bn, threads);
   if (cfg >= S2D_CFG_BASE) return sepconv_2d_config(cfg - S2D_CFG_BASE, bm, bn, threads);
   if (cfg >= SEPW_CFG_BASE) return sepconv_ws_config(cfg - SEPW_CFG_BASE, bm, bn, threads);

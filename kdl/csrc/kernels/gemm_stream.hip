@@ -1,0 +1,248 @@
+// Streaming pointwise GEMM for small K and large M (EfficientNet-B7's 1x1 expand / project convs on
+// its 300x300 / 150x150 / 75x75 maps: K 32-480, N 32-480, M up to 2.9 M rows per batch of 32).
+//
+// These layers are HBM-bound (a 150x150 expand writes 415 MB for 28 GFLOP), but the tiled GEMMs
+// (gemm_pipe / conv_gemm) ran them at 1.7-3.2 TB/s effective: a tile's prologue (operand DMA), a 1-2
+// step K loop and its LDS-staged epilogue are paid once per tile of a few dozen KB
+// (tools/layer_profile.py --model efficientnet_b7, round 5). Here:
+//   * persistent workgroups of 8 or 16 waves, one round of them (occupancy-sized grid); the whole weight matrix (NF fragments x KT k-steps, fragment-
+//     linear, <= 90 KiB) and the bias sit in LDS for the kernel's life (reloaded only when a
+//     workgroup's row range crosses into the next image's per-image weights, ConvGemmArgs.wimg);
+//   * every wave streams 16-row A fragments straight from HBM into registers, PD fragments ahead
+//     (register ring), so each CU keeps ~16 x PD x KT KiB of reads in flight;
+//   * per row fragment, the NF output fragments are computed two at a time (MFMA 16x16x32 with the
+//     weight fragment as the first operand: each lane holds 4 consecutive output channels of one
+//     row) and stored from the accumulators (8 bytes per lane: bias, SiLU / ReLU, residual fused) --
+//     no C tile through LDS, no barrier in the loop.
+// Instances per (KT, NF) -- the B7 shapes; any other shape is refused (hipErrorInvalidValue) and the
+// layer keeps its tiled configs.
+#include "common.h"
+#include "launch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+namespace kdl {
+
+namespace {
+
+// A fragments (and, with RES, the residual rows) each wave keeps in flight: the register ring holds
+// PD x (KT A k-steps of 4 VGPRs + NF residual pairs of 2), about 72 VGPRs at most
+template <int KT, int NF, bool RES>
+constexpr int gs_prefetch() {
+  constexpr int per = KT * 4 + (RES ? NF * 2 : 0);
+  return per * 3 <= 72 ? 3 : per * 2 <= 72 ? 2 : 1;
+}
+
+template <int KT, int NF>
+constexpr int gs_lds() { return NF * KT * 1024 + NF * 64; }
+
+// waves per workgroup: 16 when the weights take over a third of the LDS (one workgroup per CU),
+// else 8, so the CU's resident waves (set by VGPRs) come in finer steps
+template <int KT, int NF>
+constexpr int gs_waves() { return gs_lds<KT, NF>() > 53 * 1024 ? 16 : 8; }
+
+// RES: the residual add, its rows prefetched into the ring with the A fragment of the same rows (a
+// residual load issued in the epilogue would make the wave wait for every newer A load too: vmcnt
+// retires in order)
+// NT: nontemporal output stores (streaming cache policy). Measured (tools/stream_ab.py, B7 b32): a win for
+// outputs well past the 256 MB MALL (the 150x150 expands: 177 -> 138 us), a loss for ones the next layer
+// can still find cached (the residual projects: 134 -> 143 us) -- a separate config id, picked by the tuner
+template <int KT, int NF, bool RES, bool NT>
+__global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(ConvGemmArgs a) {
+  constexpr int PD = gs_prefetch<KT, NF, RES>();
+  constexpr int GS_NW = gs_waves<KT, NF>();
+  __shared__ __attribute__((aligned(16))) uint8_t sB[NF * KT * 1024];
+  __shared__ __attribute__((aligned(16))) float sBias[NF * 16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int OHW = a.OH * a.OW;
+  const int FPI = (OHW + 15) / 16;                   // 16-row fragments per image (the last may be partial)
+  const int T = a.B * FPI;
+  // A operand: lane = (row, 8-element k chunk); accumulator of fragment pair j: channels
+  // 16 j + nq .. + 7 of the same row (the permuted weight columns)
+  const int row = lane & 15, kq = lane >> 4;
+  const int nq = 8 * (lane >> 4);
+  static_assert(NF % 2 == 0, "fragment pairs");
+  // Fragment order. Shared weights: workgroups take NW-fragment chunks round-robin, so the resident
+  // grid moves through the rows as one window (DRAM pages and TLB reach shared by every CU; a
+  // contiguous slice per workgroup made ~800 separate write streams and capped wide outputs at
+  // 2.7 TB/s). Per-image weights: a contiguous slice per workgroup, walked image by image, so the
+  // weights are reloaded only where the slice crosses an image.
+  const bool il = a.wimg == 0;
+  const int f0 = (int)((long)T * blockIdx.x / gridDim.x), f1 = (int)((long)T * (blockIdx.x + 1) / gridDim.x);
+
+  for (int i = tid; i < NF * 16; i += 64 * GS_NW) sBias[i] = a.bias[i];
+  int loaded = -1;                                   // image whose weights are in sB (-1: none)
+  for (int fb = il ? 0 : f0; il ? fb == 0 : fb < f1;) {
+    const int img = il ? 0 : fb / FPI;
+    const int fend = il ? T : min(f1, (img + 1) * FPI);
+    if (loaded < 0 || (a.wimg && img != loaded)) {
+      __syncthreads();                               // the previous segment's waves are done with sB
+      const uint16_t* wsrc = a.wp + (a.wimg ? (long)img * a.wimg : 0L);
+      // fragment j, k-step t: KT consecutive KiB per fragment as in the packed [NF_pack][K/32][64][8]
+      // layout, but with the output channels permuted inside each fragment pair (j even, j + 1): column
+      // c of fragment j + h is channel 16 j + 8 (c / 4) + 4 h + c % 4, so accumulator lane quad g of the
+      // pair holds the 8 consecutive channels 16 j + 8 g .. + 7 (one 16-byte store per lane)
+      for (int i = tid; i < NF * KT * 64; i += 64 * GS_NW) {
+        const int l = i & 63, jt = i >> 6, j = jt / KT, t = jt - j * KT, c = l & 15;
+        const int ch = (j & ~1) * 16 + (c >> 2) * 8 + (j & 1) * 4 + (c & 3);
+        const int src = ((ch >> 4) * KT + t) * 64 + ((ch & 15) | (l & 48));
+        *(u32x4*)(sB + i * 16) = *(const u32x4*)(wsrc + (long)src * 8);
+      }
+      __syncthreads();
+      loaded = img;
+    }
+    // this wave's fragments: fbase + q * fstep, q < mine (wave-uniform)
+    const int fbase = il ? blockIdx.x * GS_NW + w : fb + w;
+    const int fstep = il ? gridDim.x * GS_NW : GS_NW;
+    const int mine = fend > fbase ? (fend - fbase + fstep - 1) / fstep : 0;
+    auto row_of = [&](int q, long& mlim) {           // row of this lane in the q-th fragment; image row limit
+      const int f = fbase + q * fstep, im = f / FPI;
+      mlim = (long)(im + 1) * OHW;
+      return (long)im * OHW + (long)(f - im * FPI) * 16 + row;
+    };
+    s16x8 ar[PD][KT];
+    u32x4 rr[PD][RES ? NF / 2 : 1];
+    auto fill = [&](s16x8 (&dst)[KT], u32x4 (&rdst)[RES ? NF / 2 : 1], int q) {
+      long mlim;
+      long m = row_of(q, mlim);
+      m = m < mlim ? m : mlim - 1;                   // rows past the image: clamped reads, never stored
+      const uint16_t* src = a.x + m * a.ldx + kq * 8;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) dst[t] = *(const s16x8*)(src + t * 32);
+      if constexpr (RES) {
+        const uint16_t* r = a.res + m * a.ldr;
+#pragma unroll
+        for (int j = 0; j < NF / 2; ++j) rdst[j] = *(const u32x4*)(r + min(j * 32 + nq, a.nstore - 8));
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+      if (p < mine) fill(ar[p], rr[p], p);
+    // the ring is unrolled by PD, so every slot index is a compile-time constant (a runtime index into
+    // a register array would go through scratch); slot p is refilled after its own MFMAs read it
+    for (int q0 = 0; q0 < mine; q0 += PD) {
+#pragma unroll
+      for (int p = 0; p < PD; ++p) {
+        const int q = q0 + p;
+        if (q >= mine) break;
+        long mlim;
+        const long m = row_of(q, mlim);
+        const bool mok = m < mlim;
+        // the weight fragments are loop-invariant: an opaque lane offset keeps their LDS reads inside
+        // the loop (hoisted, NF x KT fragments would take 4 x NF x KT VGPRs and spill)
+        uint32_t boff = lane * 16;
+        asm volatile("" : "+v"(boff));
+#pragma unroll
+        for (int j0 = 0; j0 < NF; j0 += 2) {
+          f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+          for (int t = 0; t < KT; ++t)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+              if (j0 + jj < NF)
+                acc[jj] = mfma16(*(const s16x8*)(sB + ((j0 + jj) * KT + t) * 1024 + boff), ar[p][t], acc[jj]);
+          const int n = j0 * 16 + nq;
+          if (!mok || n >= a.nstore) continue;
+          const float4 b0 = *(const float4*)(sBias + n), b1 = *(const float4*)(sBias + n + 4);
+          float v[8] = {acc[0][0] + b0.x, acc[0][1] + b0.y, acc[0][2] + b0.z, acc[0][3] + b0.w,
+                        acc[1][0] + b1.x, acc[1][1] + b1.y, acc[1][2] + b1.z, acc[1][3] + b1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            if (a.relu_out == 1) v[e] = fmaxf(v[e], 0.f);
+            else if (a.relu_out == 4) v[e] = fast_silu(v[e]);
+          }
+          if constexpr (RES) {
+            const u32x4 r = rr[p][j0 / 2];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[2 * e] += bf_lo(r[e]); v[2 * e + 1] += bf_hi(r[e]); }
+          }
+          if (a.relu_out == 2)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          const u32x4 o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]), pack_bf16(v[4], v[5]), pack_bf16(v[6], v[7])};
+          if constexpr (NT) __builtin_nontemporal_store(o, (u32x4*)(a.y + m * a.ldy + n));
+          else *(u32x4*)(a.y + m * a.ldy + n) = o;
+        }
+        if (q + PD < mine) fill(ar[p], rr[p], q + PD);   // refill slot p: this wave's fragment q + PD
+      }
+    }
+    fb = fend;
+  }
+}
+
+int num_cus() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+
+template <int KT, int NF, bool RES, bool NT>
+hipError_t launch_nt(const ConvGemmArgs& a, hipStream_t s) {
+  constexpr int NW = gs_waves<KT, NF>();
+  // one round of resident workgroups (by VGPRs and LDS, as the runtime computes it): a grid past
+  // that runs its excess as a tail round on a fraction of the CUs
+  static const int per_cu = [] {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gemm_stream_kernel<KT, NF, RES, NT>, 64 * NW, 0) != hipSuccess)
+      return 1;
+    return std::max(1, n);
+  }();
+  const long frags = (long)a.B * ((a.OH * a.OW + 15) / 16);
+  const long want = (frags + NW - 1) / NW;
+  const int grid = (int)std::max(1L, std::min(want, (long)num_cus() * per_cu));
+  hipLaunchKernelGGL((gemm_stream_kernel<KT, NF, RES, NT>), dim3(grid), dim3(64 * NW), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int KT, int NF, bool RES>
+hipError_t launch_stream(const ConvGemmArgs& a, bool nt, hipStream_t s) {
+  return nt ? launch_nt<KT, NF, RES, true>(a, s) : launch_nt<KT, NF, RES, false>(a, s);
+}
+
+// residual instances up to NF 18 (wider ones would spill the residual ring; no B7 layer has one)
+template <int KT, int NF>
+hipError_t launch_res(const ConvGemmArgs& a, bool nt, hipStream_t s) {
+  if constexpr (NF <= 18) return launch_stream<KT, NF, true>(a, nt, s);
+  else return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// (KT = K / 32, NF = output fragments) instances: EfficientNet-B7's large-map 1x1 convs
+#define KDL_STREAM_SHAPES(X) \
+  X(1, 2) X(2, 2) X(1, 12) X(6, 4) X(2, 18) X(9, 4) X(9, 6) X(3, 30) X(15, 6)
+
+bool gemm_stream_shape(int K, int nstore) {
+  const int kt = K / 32, nf = (nstore + 15) / 16;
+  switch (kt * 100 + nf) {
+#define KDL_GSHAS(kt_, nf_) case kt_ * 100 + nf_:
+    KDL_STREAM_SHAPES(KDL_GSHAS)
+#undef KDL_GSHAS
+    return K % 32 == 0;
+    default: return false;
+  }
+}
+
+hipError_t gemm_stream(const ConvGemmArgs& a, bool nt, hipStream_t s) {
+  if (a.dt != 0 || a.opad || a.stride != 1 || a.ksplit > 1 || a.OH != a.H || a.OW != a.W || a.M <= 0 ||
+      a.M != a.B * a.OH * a.OW || a.K % 32 != 0 || a.ldx % 8 != 0 || a.ldy % 8 != 0 || a.nstore % 8 != 0 ||
+      (a.res && a.ldr % 8 != 0) || a.wimg < 0 || !gemm_stream_shape(a.K, a.nstore) ||
+      a.relu_out == 3 || a.relu_in || a.NF * 16 < a.nstore)
+    return hipErrorInvalidValue;
+  switch ((a.K / 32) * 100 + (a.nstore + 15) / 16) {
+#define KDL_GSCASE(kt_, nf_) \
+  case kt_ * 100 + nf_: return a.res ? launch_res<kt_, nf_>(a, nt, s) : launch_stream<kt_, nf_, false>(a, nt, s);
+    KDL_STREAM_SHAPES(KDL_GSCASE)
+#undef KDL_GSCASE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace kdl

@@ -99,6 +99,12 @@ int conv3x3_2d_config(int cfg, int* bm, int* bn, int* threads);
 constexpr int S2D_CFG_BASE = 160;
 hipError_t sepconv_2d(int cfg, const ConvGemmArgs& a, hipStream_t s);
 int sepconv_2d_config(int cfg, int* bm, int* bn, int* threads);
+// cfg == STREAM_CFG_BASE (+1: nontemporal output stores): persistent streaming pointwise GEMM, weights
+// resident in LDS (MODE_PW, stride 1, small K; the (K, N) shapes of gemm_stream.hip's instance list
+// only; per-image weights ok).
+constexpr int STREAM_CFG_BASE = 3000;
+hipError_t gemm_stream(const ConvGemmArgs& a, bool nt, hipStream_t s);
+bool gemm_stream_shape(int K, int nstore);
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads);

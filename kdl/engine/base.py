@@ -18,7 +18,7 @@ from pathlib import Path
 import torch
 
 from ..ops import _lib
-from ..ops.conv import MODE_DW, ConvGemmLayer, is_splitk, splitk_parts
+from ..ops.conv import MODE_DW, STREAM_IDS, ConvGemmLayer, is_splitk, splitk_parts
 
 
 @dataclass
@@ -184,7 +184,10 @@ class EngineBase:
         return list(zip(prog.op_names(), ms))
 
     def _variants(self, step: Step) -> list[tuple[bool, int]]:
-        return step.layer.variants(step.geom[1])
+        v = step.layer.variants(step.geom[1])
+        if step.res and not getattr(step.layer, "stream_ok", lambda res=False: True)(res=True):
+            v = [x for x in v if x[1] not in STREAM_IDS]
+        return v
 
     def autotune(self, b: int, iters: int = 10, verbose: bool = False) -> dict[str, list[int]]:
         """Pick the fastest (split, tile config) per conv layer by timing on the device."""
@@ -231,6 +234,8 @@ class EngineBase:
                 continue
             split, cfg = (False, v) if isinstance(v, int) else (bool(v[0]), int(v[1]))
             ok = cfg in s.layer.candidates       # (ids 1000-1999, the retired hipBLASLt node, are refused)
+            if cfg in STREAM_IDS:
+                ok = getattr(s.layer, "stream_ok", lambda res=False: False)(res=bool(s.res))
             if is_splitk(cfg):
                 sk, base = splitk_parts(cfg)
                 ok = sk in getattr(s.layer, "ksplit", ()) and base in s.layer.candidates

@@ -81,6 +81,14 @@ SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
 # ids >= SPLITK_BASE: an LDS-DMA GEMM config (16..63) with K split over ksplit workgroups per tile
 # (gemm_pipe.hip ConvGemmArgs.ksplit): SPLITK_BASE + 100 * ksplit + base id
 SPLITK_BASE = 2000
+# STREAM_BASE: persistent streaming pointwise GEMM with the weights resident in LDS (gemm_stream.hip;
+# MODE_PW stride 1, bf16; only the (K/32, ldy/16) instances in STREAM_SHAPES -- EfficientNet-B7's
+# large-map expand / project convs). Stores all ldy channels, so its nominal tile is 16 x 32.
+# STREAM_NT: the same with nontemporal output stores (outputs far past the 256 MB MALL).
+STREAM_BASE = 3000
+STREAM_NT = 3001
+STREAM_IDS = (STREAM_BASE, STREAM_NT)
+STREAM_SHAPES = frozenset([(1, 2), (2, 2), (1, 12), (6, 4), (2, 18), (9, 4), (9, 6), (3, 30), (15, 6)])
 # never autotune candidates: the ws stamping build and band ablation
 ABLATION_IDS = frozenset([127, 147])
 
@@ -113,7 +121,7 @@ def config_applicable(cfg: int, W: int | None, K: int | None = None, n: int | No
 
 
 def is_splitk(cfg: int) -> bool:
-    return cfg >= SPLITK_BASE
+    return SPLITK_BASE <= cfg < STREAM_BASE
 
 
 def splitk_parts(cfg: int) -> tuple[int, int]:
@@ -127,6 +135,8 @@ def splitk_id(ksplit: int, base: int) -> int:
 
 
 def cfg_tile(cfg: int) -> tuple[int, int]:
+    if cfg in STREAM_IDS:
+        return 16, 32
     if is_splitk(cfg):
         cfg = splitk_parts(cfg)[1]
     fm, fn, wgm, wgn = CONFIGS[cfg]
@@ -231,11 +241,21 @@ class ConvGemmLayer:
             return [(False, c) for c in self.candidates
                     if c < SEP_BASE or (c >= C3_BASE and self.stride == 1 and config_applicable(c, W, self.K, self.n))] + skv
         if self.mode != MODE_DW:
-            return [(False, c) for c in self.candidates if c < SEP_BASE] + skv
+            return ([(False, c) for c in self.candidates if c < SEP_BASE] + skv
+                    + ([(False, c) for c in STREAM_IDS] if self.stream_ok() else []))
         # separable conv: fused configs, or the split lowering (depthwise, then a plain GEMM -- split-K too)
         return ([(False, c) for c in self.candidates
                  if (c < PIPE_BASE or c >= SEP_BASE) and config_applicable(c, W, self.K, self.n)]
                 + [(True, c) for c in self.candidates if c < SEP_BASE] + [(True, c) for _, c in skv])
+
+    def stream_ok(self, res: bool = False) -> bool:
+        """The streaming GEMM has an instance for this layer (host mirror of gemm_stream's checks;
+        the packed weights must hold all ldy / 16 fragments; residual instances up to ldy 288)."""
+        if res and self.ldy > 288:
+            return False
+        return (self.mode == MODE_PW and self.stride == 1 and self.dt == 0 and not self.relu_in
+                and self.relu_out != 3 and (self.K // 32, self.ldy // 16) in STREAM_SHAPES
+                and self.nf_max * 16 >= self.ldy)
 
     def dw_args(self, x: int, tmp: int, g: Geometry, ldx: int | None = None) -> dict:
         assert (ldx or self.cin_pad) == self.cin_pad
@@ -283,7 +303,8 @@ class ConvGemmLayer:
             return
         ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
         if wimg:
-            assert PIPE_BASE <= cfg < SEP_BASE, "per-image weights ride the LDS-DMA pipelined GEMM"
+            assert PIPE_BASE <= cfg < SEP_BASE or cfg in STREAM_IDS, \
+                "per-image weights ride the LDS-DMA pipelined GEMM or the streaming GEMM"
             ga.update(wp=wimg[0], wimg=wimg[1])
         if prog is None:
             C.conv_gemm(self.mode, cfg, ga, _lib.stream_ptr())

@@ -302,6 +302,82 @@ def test_per_image_weights_fold_channel_scale(HW, K, N):
             raise AssertionError(f"cfg={cfg}: {e}") from None
 
 
+# (K, n) of every streaming-GEMM instance (EfficientNet-B7's large-map expand / project convs)
+STREAM_KN = [(32, 32), (64, 32), (32, 192), (192, 48), (64, 288), (288, 48), (288, 80), (96, 480), (480, 80)]
+
+
+@pytest.mark.parametrize("K,N", STREAM_KN)
+@pytest.mark.parametrize("kind", ["silu", "wimg_res"])
+@pytest.mark.parametrize("nt", [False, True])
+def test_gemm_stream(K, N, kind, nt):
+    """Streaming pointwise GEMM (gemm_stream.hip, id STREAM_BASE) against the fp32 reference: the
+    expand form (SiLU epilogue, shared weights) and the project form (per-image SE-scaled weights,
+    residual add), on a ragged 37x37 map (partial 16-row fragments, images crossing workgroups);
+    both the plain and the nontemporal-store ids."""
+    from kdl.ops.conv import STREAM_BASE, STREAM_NT
+    cfg = STREAM_NT if nt else STREAM_BASE
+    gen = torch.Generator().manual_seed(K * 7 + N)
+    B, H = 3, 37
+    lay = _layer(MODE_PW, K, N, gen)
+    assert lay.stream_ok() and (False, cfg) in lay.variants(H)
+    g = Geometry(B, H, H, H, H)
+    x = _rand_act((B, H, H), lay.cin_pad, K, gen)
+    y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    if kind == "silu":
+        ref = conv_gemm_ref(lay, x, g)
+        ref[:, :N] = torch.nn.functional.silu(ref[:, :N])
+        lay.relu_out = 4
+        lay.launch(x, y, g, cfg=cfg)
+    else:
+        # (residual instances stop at ldy 288: wider ones are refused, and the engine never offers them)
+        res = _rand_act((B, H, H), lay.ldy, N, gen) if lay.stream_ok(res=True) else None
+        sc = (torch.rand(B, K, generator=gen) + 0.25).to(DEV)
+        xs = (x.float().view(B, H * H, lay.cin_pad) * sc[:, None, :]).to(torch.bfloat16).contiguous()
+        ref = conv_gemm_ref(lay, xs.view(-1), g, res=res)
+        per = lay.wp.numel()
+        wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
+        _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B, NF=lay.nf_max,
+                                     KT=lay.K // 32, C=K), _lib.stream_ptr())
+        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, res=_lib.ptr(res) if res is not None else None, cfg=cfg,
+                 wimg=(_lib.ptr(wimg), per))
+    torch.cuda.synchronize()
+    _check(y, ref, N, tol=3e-2)
+
+
+@pytest.mark.parametrize("K,N", [(32, 32), (288, 80)])
+def test_gemm_stream_persistent(K, N):
+    """300x300 maps: more 16-row fragments than the persistent grid's waves, so every wave walks
+    several fragments through its register ring (and the per-CU LDS budget sets the grid)."""
+    from kdl.ops.conv import STREAM_BASE
+    gen = torch.Generator().manual_seed(K + N)
+    B, H = 3 if K == 32 else 2, 300
+    lay = _layer(MODE_PW, K, N, gen)
+    g = Geometry(B, H, H, H, H)
+    x = _rand_act((B, H, H), lay.cin_pad, K, gen)
+    ref = conv_gemm_ref(lay, x, g)
+    ref[:, :N] = torch.nn.functional.silu(ref[:, :N])
+    lay.relu_out = 4
+    y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
+    lay.launch(x, y, g, cfg=STREAM_BASE)
+    torch.cuda.synchronize()
+    _check(y, ref, N, tol=3e-2)
+
+
+def test_gemm_stream_refuses_wide_residual():
+    """Residual instances stop at ldy 288: a wider one is refused loudly, not run wrong."""
+    from kdl.ops.conv import STREAM_BASE
+    gen = torch.Generator().manual_seed(3)
+    lay = _layer(MODE_PW, 96, 480, gen)
+    g = Geometry(1, 8, 8, 8, 8)
+    x = _rand_act((1, 8, 8), lay.cin_pad, 96, gen)
+    res = _rand_act((1, 8, 8), lay.ldy, 480, gen)
+    y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+    assert not lay.stream_ok(res=True)
+    with pytest.raises(RuntimeError):
+        lay.launch(x, y, g, res=res, cfg=STREAM_BASE)
+        torch.cuda.synchronize()
+
+
 def test_head():
     gen = torch.Generator().manual_seed(7)
     B, HW, F_, H1, NC = 5, 100, 2048, 100, 10
