@@ -27,7 +27,7 @@ def main():
     import torch
     from kdl.engine import registry
     from kdl.engine.tuning import tuning_path
-    from kdl.ops.conv import STREAM_BASE, STREAM_NT
+    from kdl.ops.conv import MODE_DW, STREAM_BASE, STREAM_NT
     info = registry.get(a.model)
     e = info.engine(info.init_params(0), a.batch, torch.device("cuda", 0))
     tp = tuning_path(info.tuning or a.model, a.batch)
@@ -38,16 +38,16 @@ def main():
     new = dict(tun)
     tot_old = tot_new = 0.0
 
-    def timeit(step, cfg):
+    def timeit(step, cfg, split):
         ts = []
         with torch.cuda.stream(s):
             for _ in range(2):
-                e._emit_conv(None, step, a.batch, cfg=cfg)
+                e._emit_conv(None, step, a.batch, split=split, cfg=cfg)
             for _ in range(a.reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
                 for _ in range(a.iters):
-                    e._emit_conv(None, step, a.batch, cfg=cfg)
+                    e._emit_conv(None, step, a.batch, split=split, cfg=cfg)
                 e1.record(s)
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3 / a.iters)
@@ -55,21 +55,22 @@ def main():
 
     for step in e.conv_steps():
         lay = step.layer
-        if not getattr(lay, "stream_ok", lambda: False)() or lay.split:
+        if not getattr(lay, "stream_ok", lambda: False)():
             continue
+        ssplit = lay.mode == MODE_DW          # separable convs: the stream GEMM runs as their split lowering
         H, W, OH, OW = step.geom
         M = a.batch * OH * OW
         nbytes = 2 * M * (step.extra.get("ldx", lay.cin_pad) + lay.ldy * (2 if step.res else 1))
         if step.res and not lay.stream_ok(res=True):
             continue
-        t0 = timeit(step, lay.cfg)
-        t1 = timeit(step, STREAM_BASE)
-        t2 = timeit(step, STREAM_NT)
+        t0 = timeit(step, lay.cfg, lay.split)
+        t1 = timeit(step, STREAM_BASE, ssplit)
+        t2 = timeit(step, STREAM_NT, ssplit)
         best, tb = min(((STREAM_BASE, t1), (STREAM_NT, t2)), key=lambda x: x[1])
         tot_old += t0
         tot_new += min(t0, tb)
         if tb < 0.97 * t0:
-            new[step.name] = [0, best]
+            new[step.name] = [int(ssplit), best]
         print(f"{step.name:26s} M {M:8d} K {lay.K:4d} ldy {lay.ldy:4d} cfg {lay.cfg:4d} {t0:7.1f} us "
               f"({nbytes / t0 / 1e6:5.2f} TB/s)  stream {t1:7.1f} us ({nbytes / t1 / 1e6:5.2f} TB/s)  "
               f"nt {t2:7.1f} us ({nbytes / t2 / 1e6:5.2f} TB/s)  {t0 / tb:5.2f}x", flush=True)
