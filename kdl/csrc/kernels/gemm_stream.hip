@@ -46,10 +46,14 @@ constexpr int gs_waves() { return gs_lds<KT, NF>() > 53 * 1024 ? 16 : 8; }
 // RES: the residual add, its rows prefetched into the ring with the A fragment of the same rows (a
 // residual load issued in the epilogue would make the wave wait for every newer A load too: vmcnt
 // retires in order)
+// ACT: the epilogue activation as a compile-time constant (ConvGemmArgs.relu_out 0 / 1 / 2 / 4): tested at run
+// time per element, it compiled to a chain of scalar branches per value that also kept the scheduler from
+// overlapping one fragment pair's epilogue with the next pair's LDS reads and MFMAs (2,592 v_mov_b64 and ~650
+// branches per loop body of the 150x150 expand instance).
 // NT: nontemporal output stores (streaming cache policy). Measured (tools/stream_ab.py, B7 b32): a win for
 // outputs well past the 256 MB MALL (the 150x150 expands: 177 -> 138 us), a loss for ones the next layer
 // can still find cached (the residual projects: 134 -> 143 us) -- a separate config id, picked by the tuner
-template <int KT, int NF, bool RES, bool NT>
+template <int KT, int NF, bool RES, bool NT, int ACT>
 __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(ConvGemmArgs a) {
   constexpr int PD = gs_prefetch<KT, NF, RES>();
   constexpr int GS_NW = gs_waves<KT, NF>();
@@ -151,15 +155,15 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
                         acc[1][0] + b1.x, acc[1][1] + b1.y, acc[1][2] + b1.z, acc[1][3] + b1.w};
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            if (a.relu_out == 1) v[e] = fmaxf(v[e], 0.f);
-            else if (a.relu_out == 4) v[e] = fast_silu(v[e]);
+            if constexpr (ACT == 1) v[e] = fmaxf(v[e], 0.f);
+            else if constexpr (ACT == 4) v[e] = fast_silu(v[e]);
           }
           if constexpr (RES) {
             const u32x4 r = rr[p][j0 / 2];
 #pragma unroll
             for (int e = 0; e < 4; ++e) { v[2 * e] += bf_lo(r[e]); v[2 * e + 1] += bf_hi(r[e]); }
           }
-          if (a.relu_out == 2)
+          if constexpr (ACT == 2)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
           const u32x4 o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]), pack_bf16(v[4], v[5]), pack_bf16(v[6], v[7])};
@@ -183,22 +187,33 @@ int num_cus() {
   return n;
 }
 
-template <int KT, int NF, bool RES, bool NT>
-hipError_t launch_nt(const ConvGemmArgs& a, hipStream_t s) {
+template <int KT, int NF, bool RES, bool NT, int ACT>
+hipError_t launch_act(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int NW = gs_waves<KT, NF>();
   // one round of resident workgroups (by VGPRs and LDS, as the runtime computes it): a grid past
   // that runs its excess as a tail round on a fraction of the CUs
   static const int per_cu = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gemm_stream_kernel<KT, NF, RES, NT>, 64 * NW, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gemm_stream_kernel<KT, NF, RES, NT, ACT>, 64 * NW, 0) != hipSuccess)
       return 1;
     return std::max(1, n);
   }();
   const long frags = (long)a.B * ((a.OH * a.OW + 15) / 16);
   const long want = (frags + NW - 1) / NW;
   const int grid = (int)std::max(1L, std::min(want, (long)num_cus() * per_cu));
-  hipLaunchKernelGGL((gemm_stream_kernel<KT, NF, RES, NT>), dim3(grid), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((gemm_stream_kernel<KT, NF, RES, NT, ACT>), dim3(grid), dim3(64 * NW), 0, s, a);
   return hipGetLastError();
+}
+
+template <int KT, int NF, bool RES, bool NT>
+hipError_t launch_nt(const ConvGemmArgs& a, hipStream_t s) {
+  switch (a.relu_out) {
+    case 0: return launch_act<KT, NF, RES, NT, 0>(a, s);
+    case 1: return launch_act<KT, NF, RES, NT, 1>(a, s);
+    case 2: return launch_act<KT, NF, RES, NT, 2>(a, s);
+    case 4: return launch_act<KT, NF, RES, NT, 4>(a, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int KT, int NF, bool RES>
