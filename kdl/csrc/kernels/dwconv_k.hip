@@ -290,6 +290,14 @@ static hipError_t dwt(const DwkArgs& a, hipStream_t s) {
 // overlap its own arithmetic and its LDS budget caps the CU at 1-3 workgroups.
 // Workgroup = CB chunk lanes x (256/CB) segment lanes of one (image, row band); the SE
 // partials are per workgroup (part = band x segment block x chunk block).
+// smallest divisor of P that is >= N (P itself if none is smaller)
+template <int P, int N>
+constexpr int dwv_ring() {
+  for (int d = N; d < P; ++d)
+    if (P % d == 0) return d;
+  return P;
+}
+
 template <int K, int S, int SEG, int CB, int PD>
 __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
   constexpr int R = (K + S - 1) / S;       // output rows in flight
@@ -364,22 +372,28 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
     }
   };
 
-  // rows v .. v+PD-1 are in registers (xq[0] = row v) and row v+PD is issued at the top of
-  // step v: PD rows of arithmetic cover each load's latency
-  u32x2 xq[PD + 1][NJ];
+  // Row ring of RS slots, RS the smallest divisor of the unroll period P holding PD + 1 rows: row v
+  // lives in slot v % RS (= u % RS, v0 being a multiple of P), and row v + RS - 1 is issued at the
+  // top of step v into the slot row v - 1 just left -- every slot index is a compile-time constant,
+  // so the ring never moves (the earlier xq[k] = xq[k + 1] rotation cost NJ * PD * 2 moves per row:
+  // 36 for the 5x5 kernel against its 100 FMAs). RS - 1 >= PD rows of arithmetic cover each load.
+  constexpr int RS = dwv_ring<P, PD + 1>();
+  constexpr int LA = RS - 1;                 // look-ahead (rows in flight)
+  u32x2 xq[RS][NJ];
 #pragma unroll
-  for (int k = 0; k < PD; ++k) load(k, xq[k]);
+  for (int k = 0; k < LA; ++k) load(k, xq[k]);
   for (int v0 = 0; v0 < vmax; v0 += P) {
 #pragma unroll
     for (int u = 0; u < P; ++u) {
       const int v = v0 + u;
       if (v >= vmax) break;
-      load(v + PD, xq[PD]);
+      load(v + LA, xq[(u + LA) % RS]);
+      const u32x2 (&xc)[NJ] = xq[u % RS];
       f32x2 xf[NJ][2];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        xf[j][0] = (f32x2){bf_lo(xq[0][j][0]), bf_hi(xq[0][j][0])};
-        xf[j][1] = (f32x2){bf_lo(xq[0][j][1]), bf_hi(xq[0][j][1])};
+        xf[j][0] = (f32x2){bf_lo(xc[j][0]), bf_hi(xc[j][0])};
+        xf[j][1] = (f32x2){bf_lo(xc[j][1]), bf_hi(xc[j][1])};
       }
 #pragma unroll
       for (int dy = 0; dy < K; ++dy) {
@@ -398,10 +412,6 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
           if (dy == K - 1) finish(acc[slot], ol);
         }
       }
-#pragma unroll
-      for (int k = 0; k < PD; ++k)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) xq[k][j] = xq[k + 1][j];
     }
   }
 
