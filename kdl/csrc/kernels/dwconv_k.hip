@@ -21,7 +21,9 @@ constexpr int DWK_MAXL = 8;
 
 __device__ __forceinline__ float silu(float v) { return fast_silu(v); }
 
-template <int K, int S, int SEG>
+// SILU: the activation (DwkArgs.act 2) as a compile-time constant, like the streaming GEMM's: a run-time
+// test in the store path splits it into branch blocks the scheduler cannot interleave
+template <int K, int S, int SEG, bool SILU>
 __global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int TW) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int C8 = a.C >> 3;
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(256) void dwk_kernel(DwkArgs a, int CG, int RB, int
         u32x4 out;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
-          if (a.act == 2) {
+          if constexpr (SILU) {
             f[2 * d] = silu(f[2 * d]);
             f[2 * d + 1] = silu(f[2 * d + 1]);
           }
@@ -269,7 +271,9 @@ static hipError_t dwt(const DwkArgs& a, hipStream_t s) {
   const int seg = dwt_seg(a);
 #define KDL_DWK(k, st, sg) \
   if (a.K == k && a.S == st && seg == sg) { \
-    hipLaunchKernelGGL((dwk_kernel<k, st, sg>), grid, block, smem, s, a, CG, RB, TW); return hipGetLastError(); }
+    if (a.act == 2) hipLaunchKernelGGL((dwk_kernel<k, st, sg, true>), grid, block, smem, s, a, CG, RB, TW); \
+    else hipLaunchKernelGGL((dwk_kernel<k, st, sg, false>), grid, block, smem, s, a, CG, RB, TW); \
+    return hipGetLastError(); }
 #define KDL_DWK_SEGS(k, st) KDL_DWK(k, st, 3) KDL_DWK(k, st, 4) KDL_DWK(k, st, 5) KDL_DWK(k, st, 7) KDL_DWK(k, st, 8)
   KDL_DWK_SEGS(3, 1) KDL_DWK_SEGS(3, 2) KDL_DWK_SEGS(5, 1) KDL_DWK_SEGS(5, 2)
 #undef KDL_DWK_SEGS
@@ -298,7 +302,7 @@ constexpr int dwv_ring() {
   return P;
 }
 
-template <int K, int S, int SEG, int CB, int PD>
+template <int K, int S, int SEG, int CB, int PD, bool SILU>
 __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
   constexpr int R = (K + S - 1) / S;       // output rows in flight
   constexpr int P = R * S;                 // unroll period (input rows)
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(256) void dwv_kernel(DwkArgs a, int RB) {
 #pragma unroll
     for (int o = 0; o < SEG; ++o) {
       float f0 = ac[o][0][0] + bq.x, f1 = ac[o][0][1] + bq.y, f2 = ac[o][1][0] + bq.z, f3 = ac[o][1][1] + bq.w;
-      if (a.act == 2) { f0 = silu(f0); f1 = silu(f1); f2 = silu(f2); f3 = silu(f3); }
+      if constexpr (SILU) { f0 = silu(f0); f1 = silu(f1); f2 = silu(f2); f3 = silu(f3); }
       const u32x2 out = {pack_bf16(f0, f1), pack_bf16(f2, f3)};
       if (live && w0 + o < a.OW) {
         *(u32x2*)(rp + (long)o * a.C) = out;
@@ -522,7 +526,8 @@ hipError_t dwk(const DwkArgs& a, hipStream_t s) {
   if (nblk >= (1L << 31)) return hipErrorInvalidValue;
 #define KDL_DWV1(k, st, sg, cb, pd)                                                                     \
   if (a.K == k && a.S == st && SEG == sg && CB == cb && PDv == pd) {                                  \
-    hipLaunchKernelGGL((dwv_kernel<k, st, sg, cb, pd>), dim3((unsigned)nblk), dim3(256), 0, s, a, RB); \
+    if (a.act == 2) hipLaunchKernelGGL((dwv_kernel<k, st, sg, cb, pd, true>), dim3((unsigned)nblk), dim3(256), 0, s, a, RB); \
+    else hipLaunchKernelGGL((dwv_kernel<k, st, sg, cb, pd, false>), dim3((unsigned)nblk), dim3(256), 0, s, a, RB); \
     return hipGetLastError();                                                                         \
   }
 #define KDL_DWV(k, st, sg, cb) KDL_DWV1(k, st, sg, cb, 1) KDL_DWV1(k, st, sg, cb, 3)
