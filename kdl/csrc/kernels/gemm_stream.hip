@@ -59,6 +59,10 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
   constexpr int GS_NW = gs_waves<KT, NF>();
   __shared__ __attribute__((aligned(16))) uint8_t sB[NF * KT * 1024];
   __shared__ __attribute__((aligned(16))) float sBias[NF * 16];
+  // STG: staged stores (no residual, >= 2 fragment pairs; see the epilogue): a 16 x 144-byte tile per wave
+  constexpr bool STG = !RES && NF >= 4;
+  constexpr int GS_STG = 16 * 144;
+  __shared__ __attribute__((aligned(16))) uint8_t sStg[STG ? GS_NW * GS_STG : 16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int OHW = a.OH * a.OW;
@@ -149,8 +153,9 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
               if (j0 + jj < NF)
                 acc[jj] = mfma16(*(const s16x8*)(sB + ((j0 + jj) * KT + t) * 1024 + boff), ar[p][t], acc[jj]);
           const int n = j0 * 16 + nq;
-          if (!mok || n >= a.nstore) continue;
-          const float4 b0 = *(const float4*)(sBias + n), b1 = *(const float4*)(sBias + n + 4);
+          if (!STG && (!mok || n >= a.nstore)) continue;   // STG: every lane takes part in the read-back
+          const int nb = min(n, NF * 16 - 8);                 // (bias reads stay inside sBias)
+          const float4 b0 = *(const float4*)(sBias + nb), b1 = *(const float4*)(sBias + nb + 4);
           float v[8] = {acc[0][0] + b0.x, acc[0][1] + b0.y, acc[0][2] + b0.z, acc[0][3] + b0.w,
                         acc[1][0] + b1.x, acc[1][1] + b1.y, acc[1][2] + b1.z, acc[1][3] + b1.w};
 #pragma unroll
@@ -167,8 +172,35 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
           const u32x4 o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]), pack_bf16(v[4], v[5]), pack_bf16(v[6], v[7])};
-          if constexpr (NT) __builtin_nontemporal_store(o, (u32x4*)(a.y + m * a.ldy + n));
-          else *(u32x4*)(a.y + m * a.ldy + n) = o;
+          auto gstore = [&](long mm, int nn, const u32x4& val) {
+            if constexpr (NT) __builtin_nontemporal_store(val, (u32x4*)(a.y + mm * a.ldy + nn));
+            else *(u32x4*)(a.y + mm * a.ldy + nn) = val;
+          };
+          const int pp = j0 / 2;                                // fragment pair
+          if constexpr (STG) {
+            if ((NF / 2) % 2 == 1 && pp == NF / 2 - 1) {       // odd pair count: the last pair goes direct
+              if (mok && n < a.nstore) gstore(m, n, o);
+            } else {
+              // two pairs (64 channels) of the wave's 16 rows through its LDS tile (144-byte padded rows),
+              // then 2 stores of 8 rows x 128 contiguous bytes each (full cache lines; direct: 16 rows x 64 B)
+              uint8_t* stg = sStg + w * GS_STG;
+              *(u32x4*)(stg + row * 144 + (pp & 1) * 64 + kq * 16) = o;
+              if (pp & 1) {
+                asm volatile("" ::: "memory");
+                const long mb = m - row;                        // the fragment's first row
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                  const int rr2 = k * 8 + (lane >> 3), c = lane & 7;
+                  const u32x4 val = *(const u32x4*)(stg + rr2 * 144 + c * 16);
+                  const int nn = (pp - 1) * 32 + c * 8;
+                  if (mb + rr2 < mlim && nn < a.nstore) gstore(mb + rr2, nn, val);
+                }
+                asm volatile("" ::: "memory");
+              }
+            }
+          } else {
+            gstore(m, n, o);
+          }
         }
         if (q + PD < mine) fill(ar[p], rr[p], q + PD);   // refill slot p: this wave's fragment q + PD
       }
