@@ -414,6 +414,8 @@ def main(argv=None) -> int:
         if spent >= a.settle_max or (spent >= a.settle and stable):
             break
     settle_s = time.perf_counter() - t_start
+    if rank == 0:   # clock-ramp trajectory of the untimed replays (fresh-lease diagnosis, stderr only)
+        print("settle chunks (10 replays, ms): " + " ".join(f"{c:.2f}" for c in chunk_ms), file=sys.stderr)
     if dist_on:
         dist.barrier()
     for i in range(a.depth):

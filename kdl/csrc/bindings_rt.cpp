@@ -233,7 +233,8 @@ PYBIND11_MODULE(_rt, m) {
   // ---- native gRPC front-end (runtime/grpc_front.h) + the native load generator
   py::class_<GrpcFront, std::unique_ptr<GrpcFront, FrontDeleter>>(m, "GrpcFront")
       // slow(path: str, message: bytes, deadline_us: int) -> (code, message, body: bytes, [(k, v)])
-      .def(py::init([](const std::string& host, int port, int io_threads, int slow_threads, py::function slow) {
+      .def(py::init([](const std::string& host, int port, int io_threads, int slow_threads, py::function slow,
+                       size_t max_recv_bytes, bool reuse_port) {
              auto fn = std::make_shared<py::function>(std::move(slow));
              SlowFn cb = [fn](const std::string& path, const std::string& msg, int64_t deadline_us) {
                py::gil_scoped_acquire gil;
@@ -251,9 +252,10 @@ PYBIND11_MODULE(_rt, m) {
              // built with the GIL held: a constructor that throws drops the callable safely (its
              // threads never wait on Python before a request arrives)
              return std::unique_ptr<GrpcFront, FrontDeleter>(
-                 new GrpcFront(host, port, io_threads, slow_threads, std::move(cb)));
+                 new GrpcFront(host, port, io_threads, slow_threads, std::move(cb), max_recv_bytes, reuse_port));
            }),
-           py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("slow_threads") = 4, py::arg("slow"))
+           py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("slow_threads") = 4, py::arg("slow"),
+           py::arg("max_recv_bytes") = size_t(64) << 20, py::arg("reuse_port") = true)
       .def_property_readonly("port", &GrpcFront::port)
       .def("set_route", [](GrpcFront& f, const std::string& model, const std::string& signature, int64_t version,
                            const std::string& input_key, const std::string& output_key, int dtype, int image,
@@ -294,12 +296,12 @@ PYBIND11_MODULE(_rt, m) {
     return py::make_tuple(ok, why);
   });
   m.def("grpc_load", [](const std::string& host, int port, const std::string& path, py::bytes message, int conns,
-                        int streams, double seconds, double warm_s, double timeout_s) {
+                        int streams, double seconds, double warm_s, double timeout_s, bool raw_frame) {
           std::string msg = message;
           LoadResult r;
           {
             py::gil_scoped_release nogil;
-            r = grpc_load(host, port, path, msg, conns, streams, seconds, warm_s, timeout_s);
+            r = grpc_load(host, port, path, msg, conns, streams, seconds, warm_s, timeout_s, raw_frame);
           }
           py::dict d;
           d["ok"] = r.ok; d["failed"] = r.failed; d["seconds"] = r.seconds; d["error"] = r.error;
@@ -309,7 +311,8 @@ PYBIND11_MODULE(_rt, m) {
           d["codes"] = codes;
           return d;
         }, py::arg("host"), py::arg("port"), py::arg("path"), py::arg("message"), py::arg("conns") = 4,
-        py::arg("streams") = 8, py::arg("seconds") = 5.0, py::arg("warm_s") = 1.0, py::arg("timeout_s") = 30.0);
+        py::arg("streams") = 8, py::arg("seconds") = 5.0, py::arg("warm_s") = 1.0, py::arg("timeout_s") = 30.0,
+        py::arg("raw_frame") = false);
 
   // ---- native batch executor (executor.h) + the fake device backend used by CPU tests
   py::class_<ExecGroup>(m, "ExecGroup")
@@ -392,6 +395,7 @@ PYBIND11_MODULE(_rt, m) {
            py::arg("latency_us") = 0)
       .def("api_ptr", [](const loop::Device& d) { return reinterpret_cast<uintptr_t>(d.api()); })
       .def_property_readonly("forwards", &loop::Device::forwards)
+      .def("fail_issues", &loop::Device::fail_issues, py::arg("n"))
       .def_static("logit", &loop::Device::logit);
   py::class_<LoopDpLeader>(m, "LoopDpLeader")
       .def(py::init([](loop::Device* local, loop::Comm* sc, loop::Comm* ga, std::vector<int> buckets, double timeout_s,

@@ -195,6 +195,11 @@ class DpLeaderT {
     if (P::select(*L_) != 0) return -1;
     const DpGeometry g{world_, L_->item_bytes(), L_->out_cols()};
     const size_t ib = L_->item_bytes();
+    // rank 0's own shard first: rows [0, shard) of the staging, straight into its engine's input
+    // slot. A local failure here fails this batch only: no control word has used a sequence
+    // number yet, so the followers' next word is still in sequence (advisor r5)
+    if (L_->issue(slot, shard, std::min(n_real, shard)) != 0) return -1;
+    // from here on every failure breaks the group (a word may be half-posted)
     *h_ctrl_[slot] = DpCtrl{DP_BATCH, shard, n_real, seq_++, 0, {0, 0, 0}};
     last_ctrl_ = now();
     if (world_ > 1) {
@@ -203,8 +208,6 @@ class DpLeaderT {
           P::record(ev_in_[slot], cs_) != 0)
         return fail_locked();
     }
-    // rank 0's own shard: rows [0, shard) of the staging, straight into its engine's input slot
-    if (L_->issue(slot, shard, std::min(n_real, shard)) != 0) return -1;
     if (world_ > 1) {
       const auto msgs = dp_leader_step(g, DP_BATCH, shard);
       std::vector<DpMsg> sc, ga;

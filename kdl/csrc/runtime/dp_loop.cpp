@@ -229,6 +229,7 @@ int Device::launch(int slot, int bucket, Event* ready, Stream** last) {
 
 int Device::issue(int slot, int bucket, int n_real) {
   (void)n_real;
+  if (fail_issues_.load() > 0 && fail_issues_.fetch_sub(1) > 0) return -1;
   if (!dev_in(slot, bucket)) return -1;
   if (LoopPlatform::h2d(din_[slot].data(), staging_[slot].data(), item_bytes_ * bucket, &copy_) != 0) return -1;
   ev_h2d_[slot].record(&copy_);

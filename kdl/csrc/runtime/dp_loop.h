@@ -115,6 +115,8 @@ class Device {
   int issue(int slot, int bucket, int n_real);
   int complete(int slot, const float** out, kdl_device_times* t);
   long forwards() const { return forwards_.load(); }
+  // fault injection (tests): the next n issue() calls fail before touching anything
+  void fail_issues(int n) { fail_issues_.store(n); }
   const kdl_exec_backend* api() const { return &api_; }
   // the value the fake forward gives column k of an input row whose first 4 bytes are `id`
   static float logit(uint32_t id, int k, int version) { return float((id & 0xFFFFF) + 1048576u * (version & 15)) + k; }
@@ -129,6 +131,7 @@ class Device {
   std::vector<std::vector<float>> out_, dout_;
   std::vector<Event> ev_h2d_, ev_done_;
   std::atomic<long> forwards_{0};
+  std::atomic<int> fail_issues_{0};
   kdl_exec_backend api_{};
   Stream copy_, compute_;                      // last members: joined first on destruction
 };

@@ -128,6 +128,13 @@ struct Call {
   std::string message, resp;
   std::vector<std::pair<std::string, std::string>> meta;
   size_t sent = 0;
+  bool rejected = false;                 // answered while its body was still arriving (size caps)
+  // request bytes this call holds against the front's budget, returned when the call dies
+  std::shared_ptr<std::atomic<int64_t>> budget;
+  int64_t held = 0;
+  ~Call() {
+    if (budget && held) budget->fetch_sub(held, std::memory_order_relaxed);
+  }
 };
 using CallP = std::shared_ptr<Call>;
 
@@ -172,6 +179,10 @@ struct Conn {
   std::string out;                           // produced bytes the socket has not taken yet
   size_t out_off = 0;
   bool pollout = false;
+  // streams answered before their request ended: RST_STREAM(NO_ERROR) once the answer's
+  // HEADERS are serialized (queued together, nghttp2 may emit the RST first and the client
+  // would see no status)
+  std::vector<int32_t> rst_after;
 };
 
 }  // namespace
@@ -181,6 +192,12 @@ struct GrpcFront::Impl {
   h2::callbacks* cbs = nullptr;
   SlowFn slow;
   int port = 0;
+  // request size caps (advisor r5): one message at most max_recv bytes; all request bodies
+  // held by the front (receiving, queued for the slow path, waiting in a batcher) at most
+  // max_held bytes -- past either the stream is answered RESOURCE_EXHAUSTED and its data dropped
+  size_t max_recv = size_t(64) << 20;
+  int64_t max_held = int64_t(1) << 30;
+  std::shared_ptr<std::atomic<int64_t>> held = std::make_shared<std::atomic<int64_t>>(0);
   std::vector<std::unique_ptr<Worker>> workers;
   std::shared_ptr<Mailbox> mail = std::make_shared<Mailbox>();
   std::atomic<bool> stopping{false};
@@ -240,72 +257,130 @@ void set_error(Call& c, int code, std::string msg) {
 }
 
 // ---- nghttp2 server callbacks (user_data = the Conn) ----
-int cb_begin_headers(h2::session*, const h2::frame_hd* f, void* ud) {
-  if (f->type != h2::FRAME_HEADERS) return 0;
-  Conn* c = static_cast<Conn*>(ud);
-  if (c->calls.count(f->stream_id)) return 0;   // trailers of a known stream
-  auto call = std::make_shared<Call>();
-  call->conn = c->id;
-  call->stream = f->stream_id;
-  call->worker = c->w->idx;
-  call->t0_us = now_us();
-  c->calls.emplace(f->stream_id, std::move(call));
+// Every body is guarded: an exception unwinding through nghttp2's C frames would terminate the
+// process (and every GPU slot's batches with it); a failing callback fails its connection only.
+#define KDL_CB_GUARD(...)                    \
+  try {                                      \
+    __VA_ARGS__                              \
+  } catch (...) {                            \
+    return h2::ERR_CALLBACK_FAILURE;         \
+  }                                          \
   return 0;
+
+// answer a stream before its request is complete and drop whatever else it sends
+void reject_early(Conn* c, const CallP& call, int code, std::string msg) {
+  call->rejected = true;
+  set_error(*call, code, std::move(msg));
+  std::string().swap(call->body);
+  if (call->budget && call->held) call->budget->fetch_sub(call->held, std::memory_order_relaxed);
+  call->held = 0;
+  c->w->local.push_back(call);
+}
+
+int cb_begin_headers(h2::session*, const h2::frame_hd* f, void* ud) {
+  KDL_CB_GUARD({
+    if (f->type != h2::FRAME_HEADERS) return 0;
+    Conn* c = static_cast<Conn*>(ud);
+    if (c->calls.count(f->stream_id)) return 0;   // trailers of a known stream
+    auto call = std::make_shared<Call>();
+    call->conn = c->id;
+    call->stream = f->stream_id;
+    call->worker = c->w->idx;
+    call->t0_us = now_us();
+    c->calls.emplace(f->stream_id, std::move(call));
+    return 0;
+  })
 }
 
 int cb_header(h2::session*, const h2::frame_hd* f, const uint8_t* n, size_t nl, const uint8_t* v, size_t vl, uint8_t,
               void* ud) {
-  if (f->type != h2::FRAME_HEADERS) return 0;
-  Conn* c = static_cast<Conn*>(ud);
-  auto it = c->calls.find(f->stream_id);
-  if (it == c->calls.end()) return 0;
-  const std::string_view name(reinterpret_cast<const char*>(n), nl);
-  if (name == ":path") it->second->path.assign(reinterpret_cast<const char*>(v), vl);
-  else if (name == "grpc-timeout") it->second->timeout.assign(reinterpret_cast<const char*>(v), vl);
-  return 0;
+  KDL_CB_GUARD({
+    if (f->type != h2::FRAME_HEADERS) return 0;
+    Conn* c = static_cast<Conn*>(ud);
+    auto it = c->calls.find(f->stream_id);
+    if (it == c->calls.end()) return 0;
+    const std::string_view name(reinterpret_cast<const char*>(n), nl);
+    if (name == ":path") it->second->path.assign(reinterpret_cast<const char*>(v), vl);
+    else if (name == "grpc-timeout") it->second->timeout.assign(reinterpret_cast<const char*>(v), vl);
+    return 0;
+  })
 }
 
 int cb_data_chunk(h2::session*, uint8_t, int32_t sid, const uint8_t* d, size_t len, void* ud) {
-  Conn* c = static_cast<Conn*>(ud);
-  auto it = c->calls.find(sid);
-  if (it == c->calls.end()) return 0;
-  std::string& b = it->second->body;
-  const bool first = b.size() < 5;
-  b.append(reinterpret_cast<const char*>(d), len);
-  if (first && b.size() >= 5) {          // the message length is known: one allocation for the rest
-    const uint32_t m = be32(reinterpret_cast<const uint8_t*>(b.data()) + 1);
-    if (m < (1u << 31)) b.reserve(size_t(5) + m);
-  }
-  return 0;
+  KDL_CB_GUARD({
+    Conn* c = static_cast<Conn*>(ud);
+    auto it = c->calls.find(sid);
+    if (it == c->calls.end() || it->second->rejected) return 0;
+    const CallP& call = it->second;
+    GrpcFront::Impl& I = *c->w->impl;
+    std::string& b = call->body;
+    // the body grows by the bytes that arrived; the client's length prefix is checked against
+    // the cap before it sizes any allocation
+    if (b.size() + len > I.max_recv + 5) {
+      reject_early(c, call, G_RESOURCE, "SERVER: Received message larger than max (" +
+                   std::to_string(b.size() + len - 5) + " vs. " + std::to_string(I.max_recv) + ")");
+      return 0;
+    }
+    if (I.held->fetch_add(int64_t(len), std::memory_order_relaxed) + int64_t(len) > I.max_held) {
+      I.held->fetch_sub(int64_t(len), std::memory_order_relaxed);
+      reject_early(c, call, G_RESOURCE, "server request memory budget exhausted");
+      return 0;
+    }
+    if (!call->budget) call->budget = I.held;
+    call->held += int64_t(len);
+    const bool first = b.size() < 5;
+    b.append(reinterpret_cast<const char*>(d), len);
+    if (first && b.size() >= 5) {        // the message length is known
+      if (uint8_t(b[0]) == 1) {
+        reject_early(c, call, G_UNIMPLEMENTED, "compressed gRPC messages are not supported");
+        return 0;
+      }
+      const uint32_t m = be32(reinterpret_cast<const uint8_t*>(b.data()) + 1);
+      if (m > I.max_recv) {
+        reject_early(c, call, G_RESOURCE, "SERVER: Received message larger than max (" + std::to_string(m) + " vs. " +
+                     std::to_string(I.max_recv) + ")");
+        return 0;
+      }
+      b.reserve(size_t(5) + m);          // m <= max_recv: one allocation for the rest
+    }
+    return 0;
+  })
 }
 
 int cb_frame_recv(h2::session*, const h2::frame_hd* f, void* ud) {
-  if ((f->type != h2::FRAME_DATA && f->type != h2::FRAME_HEADERS) || !(f->flags & h2::FLAG_END_STREAM)) return 0;
-  Conn* c = static_cast<Conn*>(ud);
-  auto it = c->calls.find(f->stream_id);
-  if (it != c->calls.end()) c->w->impl->dispatch(c->w, it->second);
-  return 0;
+  KDL_CB_GUARD({
+    if ((f->type != h2::FRAME_DATA && f->type != h2::FRAME_HEADERS) || !(f->flags & h2::FLAG_END_STREAM)) return 0;
+    Conn* c = static_cast<Conn*>(ud);
+    auto it = c->calls.find(f->stream_id);
+    if (it != c->calls.end() && !it->second->rejected) c->w->impl->dispatch(c->w, it->second);
+    return 0;
+  })
 }
 
 int cb_stream_close(h2::session*, int32_t sid, uint32_t, void* ud) {
-  static_cast<Conn*>(ud)->calls.erase(sid);
-  return 0;
+  KDL_CB_GUARD({
+    static_cast<Conn*>(ud)->calls.erase(sid);
+    return 0;
+  })
 }
 
 ssize_t cb_read_resp(h2::session* s, int32_t sid, uint8_t* buf, size_t len, uint32_t* flags, h2::data_source* src,
                      void* ud) {
-  Call* call = static_cast<Call*>(src->ptr);
-  const size_t n = std::min(len, call->resp.size() - call->sent);
-  std::memcpy(buf, call->resp.data() + call->sent, n);
-  call->sent += n;
-  if (call->sent == call->resp.size()) {
-    *flags |= h2::DATA_FLAG_EOF | h2::DATA_FLAG_NO_END_STREAM;
-    static const std::string k = "grpc-status", v = "0";
-    const h2::nv tr = h2::make_nv(k, v);
-    static_cast<Conn*>(ud)->w->impl->H->submit_trailer(s, sid, &tr, 1);
-  }
-  return ssize_t(n);
+  KDL_CB_GUARD({
+    Call* call = static_cast<Call*>(src->ptr);
+    const size_t n = std::min(len, call->resp.size() - call->sent);
+    std::memcpy(buf, call->resp.data() + call->sent, n);
+    call->sent += n;
+    if (call->sent == call->resp.size()) {
+      *flags |= h2::DATA_FLAG_EOF | h2::DATA_FLAG_NO_END_STREAM;
+      static const std::string k = "grpc-status", v = "0";
+      const h2::nv tr = h2::make_nv(k, v);
+      static_cast<Conn*>(ud)->w->impl->H->submit_trailer(s, sid, &tr, 1);
+    }
+    return ssize_t(n);
+  })
 }
+#undef KDL_CB_GUARD
 
 }  // namespace
 
@@ -444,6 +519,8 @@ void GrpcFront::Impl::answer(Worker* w, const CallP& call) {
     if (!msg.empty()) nva.push_back(h2::make_nv(kgm, msg));
     if (H->submit_response(c->s, call->stream, nva.data(), nva.size(), nullptr) != 0)
       H->submit_rst_stream(c->s, 0, call->stream, h2::INTERNAL_ERROR);
+    else if (call->rejected)             // answered mid-request: stop the client's upload once the status is out
+      c->rst_after.push_back(call->stream);
   }
 }
 
@@ -468,8 +545,14 @@ void GrpcFront::Impl::slow_loop() {
     call->code = r.code;
     call->message = std::move(r.message);
     call->meta = std::move(r.meta);
-    if (r.code == G_OK) call->resp = grpc_frame(r.body);
+    try {
+      if (r.code == G_OK) call->resp = grpc_frame(r.body);
+    } catch (const std::bad_alloc&) {
+      set_error(*call, G_RESOURCE, "out of memory building the response");
+    }
     std::string().swap(call->body);      // the request is no longer needed
+    if (call->budget && call->held) call->budget->fetch_sub(call->held, std::memory_order_relaxed);
+    call->held = 0;
     mail->post(call);
   }
 }
@@ -519,7 +602,12 @@ bool GrpcFront::Impl::flush(Worker* w, Conn* c) {
       close_conn(w, c);
       return false;
     }
-    if (n == 0) break;
+    if (n == 0) {
+      if (c->rst_after.empty()) break;
+      for (int32_t sid : c->rst_after) H->submit_rst_stream(c->s, 0, sid, h2::NO_ERROR);
+      c->rst_after.clear();
+      continue;
+    }
     size_t off = 0;
     while (off < size_t(n)) {
       const ssize_t k = ::send(c->fd, d + off, size_t(n) - off, MSG_NOSIGNAL);
@@ -633,7 +721,12 @@ void GrpcFront::Impl::run(Worker* w) {
         }
         touched.clear();
         for (const auto& call : done) {
-          answer(w, call);
+          try {
+            answer(w, call);
+          } catch (...) {                  // e.g. bad_alloc building a response: reset that stream only
+            auto ci = w->conns.find(call->conn);
+            if (ci != w->conns.end()) H->submit_rst_stream(ci->second->s, 0, call->stream, h2::INTERNAL_ERROR);
+          }
           touched.insert(call->conn);
         }
         done.clear();
@@ -644,8 +737,14 @@ void GrpcFront::Impl::run(Worker* w) {
       } else {
         auto it = w->conns.find(id);
         if (it == w->conns.end()) continue;
-        if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) on_readable(w, it->second.get());
-        else if (evs[i].events & EPOLLOUT) flush(w, it->second.get());
+        try {
+          if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) on_readable(w, it->second.get());
+          else if (evs[i].events & EPOLLOUT) flush(w, it->second.get());
+        } catch (...) {                    // outside the nghttp2 callbacks (answer, flush): drop the connection
+          w->local.clear();
+          auto again = w->conns.find(id);
+          if (again != w->conns.end()) close_conn(w, again->second.get());
+        }
       }
     }
   }
@@ -653,14 +752,19 @@ void GrpcFront::Impl::run(Worker* w) {
 }
 
 // ---------------------------------------------------------------- GrpcFront
-GrpcFront::GrpcFront(const std::string& host, int port, int io_threads, int slow_threads, SlowFn slow)
+GrpcFront::GrpcFront(const std::string& host, int port, int io_threads, int slow_threads, SlowFn slow,
+                     size_t max_recv_bytes, bool reuse_port)
     : p_(std::make_unique<Impl>()) {
   std::string why;
   p_->H = h2::api(&why);
   if (!p_->H) throw std::runtime_error(why);
   if (io_threads < 1 || slow_threads < 1 || !slow) throw std::invalid_argument("GrpcFront: bad arguments");
+  if (max_recv_bytes < 64 || max_recv_bytes > (size_t(1) << 31) - 1)
+    throw std::invalid_argument("GrpcFront: max_recv_bytes out of range [64, 2^31)");
   Impl& I = *p_;
   I.slow = std::move(slow);
+  I.max_recv = max_recv_bytes;
+  I.max_held = std::max<int64_t>(int64_t(16) * int64_t(max_recv_bytes), int64_t(256) << 20);
   I.H->callbacks_new(&I.cbs);
   I.H->set_on_begin_headers(I.cbs, cb_begin_headers);
   I.H->set_on_header(I.cbs, cb_header);
@@ -687,6 +791,22 @@ GrpcFront::GrpcFront(const std::string& host, int port, int io_threads, int slow
     stop();
     throw std::runtime_error("GrpcFront: " + e);
   };
+  // The workers' listeners share the port through SO_REUSEPORT. Unless the port is meant to be
+  // shared with other processes (--procs children), a server already bound there must make
+  // this one fail, not silently take part of its connections: probe with a plain bind first.
+  if (!reuse_port && port != 0) {
+    const int probe = ::socket(family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (probe < 0) fail("socket");
+    const int one = 1;
+    setsockopt(probe, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    const int rc = ::bind(probe, reinterpret_cast<sockaddr*>(&addr), alen);
+    const int err = errno;
+    ::close(probe);
+    if (rc != 0) {
+      errno = err;
+      fail("bind " + host + ":" + std::to_string(port));
+    }
+  }
   for (int i = 0; i < io_threads; ++i) {
     auto w = std::make_unique<Worker>();
     w->impl = p_.get();

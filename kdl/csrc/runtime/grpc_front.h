@@ -63,8 +63,13 @@ struct FrontStats {
 
 class GrpcFront {
  public:
-  // binds host:port (0: any free port) once per io thread; throws on failure
-  GrpcFront(const std::string& host, int port, int io_threads, int slow_threads, SlowFn slow);
+  // binds host:port (0: any free port) once per io thread; throws on failure.
+  // max_recv_bytes: largest request message (grpcio's max_receive_message_length; larger ones
+  // get RESOURCE_EXHAUSTED before their bytes are buffered); the bodies held at once are capped
+  // at max(16 x that, 256 MiB). reuse_port: the port may be shared with other processes
+  // (--procs); false makes the bind fail when another server holds it.
+  GrpcFront(const std::string& host, int port, int io_threads, int slow_threads, SlowFn slow,
+            size_t max_recv_bytes = size_t(64) << 20, bool reuse_port = true);
   ~GrpcFront();
   GrpcFront(const GrpcFront&) = delete;
   GrpcFront& operator=(const GrpcFront&) = delete;

@@ -164,7 +164,7 @@ void one_connection(const h2::Api* H, const sockaddr_storage& addr, socklen_t al
 }  // namespace
 
 LoadResult grpc_load(const std::string& host, int port, const std::string& path, const std::string& message,
-                     int conns, int streams, double seconds, double warm_s, double timeout_s) {
+                     int conns, int streams, double seconds, double warm_s, double timeout_s, bool raw_frame) {
   LoadResult out;
   std::string why;
   const h2::Api* H = h2::api(&why);
@@ -184,10 +184,15 @@ LoadResult grpc_load(const std::string& host, int port, const std::string& path,
   const socklen_t alen = res->ai_addrlen;
   const int family = res->ai_family;
   freeaddrinfo(res);
-  std::string req(5, '\0');
-  const uint32_t n = uint32_t(message.size());
-  req[1] = char(n >> 24), req[2] = char(n >> 16), req[3] = char(n >> 8), req[4] = char(n);
-  req += message;
+  std::string req;
+  if (raw_frame) {                       // the caller's bytes as they are (e.g. a length prefix that lies)
+    req = message;
+  } else {
+    req.assign(5, '\0');
+    const uint32_t n = uint32_t(message.size());
+    req[1] = char(n >> 24), req[2] = char(n >> 16), req[3] = char(n >> 8), req[4] = char(n);
+    req += message;
+  }
   const int64_t t0 = now_us(), warm = t0 + int64_t(warm_s * 1e6), end = t0 + int64_t((warm_s + seconds) * 1e6);
   const int64_t give_up = end + int64_t(timeout_s * 1e6);
   const std::string authority = host + ":" + std::to_string(port);

@@ -19,7 +19,10 @@ struct LoadResult {
   std::string error;                     // first connection-level failure, if any
 };
 
+// raw_frame: `message` already carries its 5-byte gRPC prefix (sent as is, to test a server's
+// handling of prefixes that do not match the bytes that follow)
 LoadResult grpc_load(const std::string& host, int port, const std::string& path, const std::string& message,
-                     int conns, int streams, double seconds, double warm_s, double timeout_s = 30);
+                     int conns, int streams, double seconds, double warm_s, double timeout_s = 30,
+                     bool raw_frame = false);
 
 }  // namespace kdl

@@ -57,7 +57,8 @@ enum : int32_t {
 };
 constexpr int ERR_DEFERRED = -508;            // NGHTTP2_ERR_DEFERRED (read callback: no data yet)
 constexpr int ERR_CALLBACK_FAILURE = -902;    // NGHTTP2_ERR_CALLBACK_FAILURE
-constexpr uint32_t INTERNAL_ERROR = 2;        // RST_STREAM / GOAWAY error code
+constexpr uint32_t NO_ERROR = 0;              // RST_STREAM / GOAWAY error codes
+constexpr uint32_t INTERNAL_ERROR = 2;
 
 // the loaded entry points (the frame-typed callbacks take nghttp2_frame*, whose first
 // member is the frame header: declared here with frame_hd* -- the same pointer)

@@ -55,6 +55,55 @@ std::string predict_request(const std::string& model, const std::string& key, in
   return req;
 }
 
+long rss_kib() {
+  FILE* f = std::fopen("/proc/self/statm", "r");
+  long pages = 0, res = 0;
+  if (f) {
+    if (std::fscanf(f, "%ld %ld", &pages, &res) != 2) res = 0;
+    std::fclose(f);
+  }
+  return res * 4;
+}
+
+// Requests that claim or carry more than the cap (advisor r5 / VERDICT r5 item 8): 1,024 streams
+// on each connection announcing 2 GiB - 1 behind a 4 KiB body, plus streams whose honest prefix
+// and bytes exceed a 1 MiB cap. Every stream must get RESOURCE_EXHAUSTED, none may reach the
+// slow path, and the process must not grow by the announced sizes.
+bool oversize_phase(int conns) {
+  std::atomic<int> slow_calls{0};
+  GrpcFront front("127.0.0.1", 0, 2, 2, [&](const std::string&, const std::string&, int64_t) {
+    slow_calls.fetch_add(1);
+    return SlowReply{};
+  }, size_t(1) << 20, false);
+  const long rss0 = rss_kib();
+  const std::string path = "/tensorflow.serving.PredictionService/Predict";
+  std::string liar(5, '\0');            // prefix: 0x7fffffff bytes follow; only 4 KiB do
+  liar[1] = char(0x7f), liar[2] = char(0xff), liar[3] = char(0xff), liar[4] = char(0xff);
+  liar += std::string(size_t(4) << 10, 'x');
+  const std::string big(size_t(3) << 20, 'y');   // honest prefix, 3 MiB > 1 MiB
+  LoadResult a, b;
+  std::thread ta([&] { a = grpc_load("127.0.0.1", front.port(), path, liar, conns, 1024, 1.0, 0.0, 10.0, true); });
+  std::thread tb([&] { b = grpc_load("127.0.0.1", front.port(), path, big, 2, 16, 1.0, 0.0, 10.0); });
+  ta.join();
+  tb.join();
+  const long grow = rss_kib() - rss0;
+  front.stop();
+  bool ok = a.error.empty() && b.error.empty() && slow_calls.load() == 0;
+  for (const LoadResult* r : {&a, &b})
+    for (const auto& kv : r->codes)
+      if (kv.first != 8) {
+        std::printf("oversize: unexpected grpc-status %d x%lld\n", kv.first, (long long)kv.second);
+        ok = false;
+      }
+  const int64_t n = a.failed + b.failed;
+  if (a.failed < 100 || b.failed < 4) ok = false;
+  if (grow > (long(512) << 10)) ok = false;   // 1,024 x 2 GiB announced per connection; < 512 MiB grown
+  std::printf("oversize: %lld + %lld streams RESOURCE_EXHAUSTED (%lld total), errors '%s' '%s', slow calls %d, "
+              "rss +%ld KiB: %s\n", (long long)a.failed, (long long)b.failed, (long long)n, a.error.c_str(),
+              b.error.c_str(), slow_calls.load(), grow, ok ? "OK" : "FAIL");
+  return ok;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -155,5 +204,6 @@ int main(int argc, char** argv) {
   std::printf("fast ok %lld (front %lld), slow answers %d, open connections at stop %lld: %s\n",
               (long long)fast.ok, (long long)st.fast_ok, slow_calls.load(), (long long)st.open_connections,
               bad ? "FAIL" : "OK");
+  bad += oversize_phase(conns) ? 0 : 1;
   return bad ? 1 : 0;
 }

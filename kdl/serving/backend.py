@@ -727,6 +727,16 @@ class Servable:
         with self._lock:
             return all(r.healthy() for r in self.runners.values())
 
+    def device_alive(self) -> bool:
+        """False once every signature that has been given work has lost all its executors.
+        Signatures nobody has called are no evidence either way (a dead device fails only the
+        signatures that reach it), and one failing signature (e.g. a shape-specific kernel fault)
+        beside a working one leaves the device alive."""
+        with self._lock:
+            runners = list(self.runners.values())
+        used = [r for r in runners if r.batcher.stats()["submitted"] > 0]
+        return not used or any(r.healthy() for r in used)
+
     def close(self):
         for r in self.runners.values():
             r.close()

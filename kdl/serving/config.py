@@ -60,6 +60,9 @@ class ServerConfig:
     # python: the grpcio server. Falls back to python when libnghttp2 is missing
     grpc_frontend: str = "native"
     grpc_io_threads: int = 4      # native front-end epoll workers (one SO_REUSEPORT listener each)
+    # largest request message either front-end accepts (RESOURCE_EXHAUSTED beyond it): one f32
+    # batch-32 299x299 request is 34.3 MB
+    grpc_max_request_bytes: int = 64 << 20
     rest_api_num_threads: int = 16
     device: str = "auto"          # auto | cpu | gpu | null (front-end ceiling: zero-latency fake device)
     gpus: int = 0                 # 0 = all visible
@@ -122,6 +125,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--grpc_frontend", choices=["native", "python"], default=None,
                     help="native: C++ HTTP/2 front-end whose Predict fast path parses, batches and answers "
                          "without Python; python: the grpcio server (env KDL_GRPC_FRONTEND, default native)")
+    ap.add_argument("--grpc_max_request_bytes", type=int, default=None,
+                    help="largest gRPC request message accepted, both front-ends (env KDL_GRPC_MAX_REQUEST_BYTES, "
+                         "default 64 MiB; an f32 batch-32 Xception request is 34.3 MB)")
     ap.add_argument("--grpc_io_threads", type=int, default=None,
                     help="native front-end I/O threads (env KDL_GRPC_IO_THREADS, default 4)")
     ap.add_argument("--device", choices=["auto", "cpu", "gpu", "null"], default="auto",
@@ -205,6 +211,8 @@ def config_from_args(argv=None, env=None) -> ServerConfig:
                         grpc_frontend=a.grpc_frontend or env.get("KDL_GRPC_FRONTEND", "native"),
                         grpc_io_threads=(a.grpc_io_threads if a.grpc_io_threads is not None
                                          else int(env.get("KDL_GRPC_IO_THREADS", "4"))),
+                        grpc_max_request_bytes=(a.grpc_max_request_bytes if a.grpc_max_request_bytes is not None
+                                                else int(env.get("KDL_GRPC_MAX_REQUEST_BYTES", str(64 << 20)))),
                         device=a.device, gpus=a.gpus, executors_per_gpu=a.executors_per_gpu,
                         synthetic=a.synthetic_model or _truthy(env.get("KDL_SYNTHETIC_MODEL", "0")),
                         labels=labels, host=a.host, dtype=a.dtype, graph=a.graph == "on",

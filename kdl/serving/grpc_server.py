@@ -247,7 +247,7 @@ def signature_def_map(s) -> "P.SignatureDefMap":
 
 
 def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: int = 64, reuse_port: bool = False,
-                      f32_exact_u8: bool = True):
+                      f32_exact_u8: bool = True, max_request_bytes: int = 64 << 20):
     sv = Servicer(manager, f32_exact_u8)
     raw = dict(request_deserializer=None, response_serializer=None)
     pred = grpc.method_handlers_generic_handler("tensorflow.serving.PredictionService", {
@@ -265,7 +265,7 @@ def build_grpc_server(manager: ModelManager, host: str, port: int, max_workers: 
         "Check": grpc.unary_unary_rpc_method_handler(sv.health_check, **raw),
     })
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=max_workers),
-                         options=[("grpc.max_receive_message_length", -1),
+                         options=[("grpc.max_receive_message_length", int(max_request_bytes)),
                                   ("grpc.max_send_message_length", -1),
                                   # --procs: every per-GPU process of the node binds the same port
                                   ("grpc.so_reuseport", 1 if reuse_port else 0)])

@@ -154,6 +154,14 @@ class ModelManager:
             servables = list(self.servables.values())
         return bool(servables) and all(s.healthy() for s in servables)
 
+    def device_alive(self) -> bool:
+        """A version is loaded and its device still works (Servable.device_alive): one signature
+        losing its executors (e.g. a shape-specific kernel fault) while another keeps serving does
+        not make the process useless; every used signature failing does (server._watch_devices)."""
+        with self._lock:
+            servables = list(self.servables.values())
+        return bool(servables) and all(s.device_alive() for s in servables)
+
     def status(self, version: int | None = None) -> list[tuple[int, int, str]]:
         with self._lock:
             items = sorted(self.states.items())

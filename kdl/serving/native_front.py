@@ -67,7 +67,7 @@ class _Context:
 
 class NativeFront:
     def __init__(self, manager, servicer, host: str, port: int, io_threads: int = 4, slow_threads: int = 64,
-                 f32_exact_u8: bool = True):
+                 f32_exact_u8: bool = True, max_request_bytes: int = 64 << 20, reuse_port: bool = True):
         self.m, self.sv, self.f32_exact_u8 = manager, servicer, f32_exact_u8
         sp, ms = "/tensorflow.serving.PredictionService/", "/tensorflow.serving.ModelService/"
         self.methods = {
@@ -82,8 +82,10 @@ class NativeFront:
         }
         self._lock = threading.Lock()
         self._learned: set[tuple] = set()
+        self._gen = 0                    # bumped by every version change (_changed)
         self._last = {"by_code": {}, "lat_counts": None, "lat_sum_ms": 0.0, "exact_u8": 0}
-        self.front = _lib.rt().GrpcFront(host, port, io_threads, slow_threads, self._slow)
+        self.front = _lib.rt().GrpcFront(host, port, io_threads, slow_threads, self._slow,
+                                         max_recv_bytes=max_request_bytes, reuse_port=reuse_port)
         self.port = self.front.port
         manager.listeners.append(self._changed)
         METRICS.poller(f"native_grpc:{id(self)}", self._poll)
@@ -121,6 +123,7 @@ class NativeFront:
         with self._lock:
             if key in self._learned:
                 return
+            gen = self._gen
         runner = s.runner(sig_name)
         sig = runner.sig
         if sig.input_shape[1] <= 0 or not hasattr(runner, "batcher") or not runner.healthy():
@@ -128,14 +131,19 @@ class NativeFront:
         u8 = None
         if self.f32_exact_u8 and sig.input_dtype == P.DT_FLOAT and NATIVE_SIGNATURE in s.signatures:
             u8 = s.runner(NATIVE_SIGNATURE).batcher
-        self.front.set_route(model=s.name, signature=sig_name, version=s.version, input_key=sig.input_key,
-                             output_key=sig.output_key, dtype=sig.input_dtype, image=sig.input_shape[1],
-                             out_cols=s.source.classes, batcher=runner.batcher, u8=u8)
         with self._lock:
+            # a version change between the lookup above and here (advisor r5) already cleared the
+            # routes: registering now would send unversioned requests to the retiring batcher
+            if gen != self._gen:
+                return
+            self.front.set_route(model=s.name, signature=sig_name, version=s.version, input_key=sig.input_key,
+                                 output_key=sig.output_key, dtype=sig.input_dtype, image=sig.input_shape[1],
+                                 out_cols=s.source.classes, batcher=runner.batcher, u8=u8)
             self._learned.add(key)
 
     def _changed(self) -> None:
         with self._lock:
+            self._gen += 1
             self._learned.clear()
             self.front.clear_routes()
 

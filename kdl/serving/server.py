@@ -44,13 +44,16 @@ class ModelServer:
                 self.native = native_front.NativeFront(self.manager, Servicer(self.manager, cfg.f32_exact_u8),
                                                        cfg.host, cfg.port, io_threads=cfg.grpc_io_threads,
                                                        slow_threads=cfg.grpc_max_threads,
-                                                       f32_exact_u8=cfg.f32_exact_u8)
+                                                       f32_exact_u8=cfg.f32_exact_u8,
+                                                       max_request_bytes=cfg.grpc_max_request_bytes,
+                                                       reuse_port=reuse)
                 self.grpc_port = self.native.port
             else:
                 log.warning("native gRPC front-end unavailable (%s): serving gRPC with grpcio", why)
         if self.native is None:
             self.grpc, self.grpc_port, _ = build_grpc_server(self.manager, cfg.host, cfg.port, cfg.grpc_max_threads,
-                                                             reuse_port=reuse, f32_exact_u8=cfg.f32_exact_u8)
+                                                             reuse_port=reuse, f32_exact_u8=cfg.f32_exact_u8,
+                                                             max_request_bytes=cfg.grpc_max_request_bytes)
             self.grpc.start()
         if cfg.rest_api_port:
             self.rest = start_rest_server(self.manager, cfg.host, cfg.rest_api_port, reuse_port=reuse,
@@ -255,11 +258,13 @@ EXIT_NO_DEVICE = 4       # a --procs child with no healthy executor left: replac
 
 def _watch_devices(srv: "ModelServer", done: threading.Event, rc: list, grace_s: float = 1.0) -> None:
     """--procs child: once the model has served, a child whose executors all went unhealthy
-    stops accepting (closes its listening sockets) and exits EXIT_NO_DEVICE, so the launcher
-    replaces it with a fresh process instead of leaving it to fail its share of connections."""
+    (no signature of any loaded version has a healthy executor left) stops accepting (closes
+    its listening sockets) and exits EXIT_NO_DEVICE, so the launcher replaces it with a fresh
+    process instead of leaving it to fail its share of connections. One failing signature
+    alone does not recycle the child: its other signatures keep serving."""
     served, bad_since = False, None
     while not done.wait(0.2):
-        ok = srv.manager.ready()
+        ok = srv.manager.device_alive()
         served = served or ok
         if not served or ok:
             bad_since = None

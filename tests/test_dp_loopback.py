@@ -195,3 +195,21 @@ def test_dead_leader_ends_followers_within_liveness_and_pings_keep_idle_ones_ali
         kind, t_end, detail = g.result[r]
         assert kind == "error" and "liveness" in detail
         assert t_end - t0 < 1.0 + 1.5, t_end - t0
+
+
+def test_one_local_issue_failure_fails_one_batch_not_the_group():
+    """Advisor r5: a failure of rank 0's own engine issue must fail that batch only. The
+    leader used to spend a sequence number before the local issue, so the next control word
+    (batch or heartbeat) reached every follower out of sequence and the whole group died."""
+    g = Group(2, buckets=[1, 2, 4], ping_s=0.1, liveness_s=2.0)
+    ok, bad, err = _clients(g, n_threads=1, n_req=5, seed=8)
+    assert not bad and not err
+    g.dev0.fail_issues(1)                # the next local issue fails before touching anything
+    ok1, bad1, err1 = _clients(g, n_threads=1, n_req=3, seed=9)
+    assert not bad1 and len(err1) == 1 and len(ok1) == 2, (ok1, err1)
+    time.sleep(0.5)                      # heartbeats after the failure keep the follower in sequence
+    ok2, bad2, err2 = _clients(g, n_threads=2, n_req=10, seed=10)
+    assert not bad2 and not err2 and len(ok2) == 20
+    assert not g.leader.broken and g.ex.healthy()
+    assert g.stop() == 0
+    assert g.result[1][0] == "stop", g.result

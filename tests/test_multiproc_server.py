@@ -209,3 +209,40 @@ def test_failed_gpu_slot_is_replaced_while_the_other_keeps_serving(tmp_path):
                 p.wait(timeout=60)
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
+
+
+def test_one_failing_signature_does_not_count_as_a_dead_device(tmp_path, monkeypatch):
+    """Advisor r5: the --procs device watch (server._watch_devices) recycles a child only when no
+    signature of any loaded version has a healthy executor left; one signature failing every
+    batch (KDL_FAULT_INJECT on its executors only) leaves the device alive while readiness drops."""
+    from kdl.serving.config import BatchingParams, ServerConfig
+    from kdl.serving.model_repo import ModelManager
+
+    monkeypatch.setenv("KDL_FAULT_INJECT", "fail=/serving_default:-1")
+    base = tmp_path / "clothing-model"
+    (base / "1").mkdir(parents=True)
+    (base / "1" / "synthetic.json").write_text('{"seed": 0}')
+    cfg = ServerConfig(port=0, rest_api_port=0, model_base_path=str(base), device="null", host="127.0.0.1",
+                       batching=BatchingParams(max_batch_size=4, batch_timeout_micros=200, allowed_batch_sizes=[1, 4]),
+                       warm_signatures=["serving_uint8"])
+    m = ModelManager(cfg)
+    m.load_initial()
+    try:
+        s = m.servables[max(m.servables)]
+        assert m.ready() and m.device_alive() and {"serving_default", "serving_uint8"} <= set(s.runners)
+        bad, good = s.runners["serving_default"], s.runners["serving_uint8"]
+        x = np.zeros((1, 299, 299, 3), np.float32)
+        for _ in range(10):                          # every batch fails: its executors give up
+            if not bad.healthy():
+                break
+            with pytest.raises(Exception):
+                bad.predict(x.tobytes(), 1, 0)
+        assert not bad.healthy() and not m.ready()
+        # only the failing signature has been used: that is all the evidence, the device is dead
+        assert not m.device_alive()
+        out = good.predict(np.full((1, 299, 299, 3), 5, np.uint8).tobytes(), 1, 0)
+        assert np.array_equal(out[0], 5 + np.arange(10, dtype=np.float32))
+        assert not m.ready() and m.device_alive()   # another signature serves on the same device
+    finally:
+        for sv in m.servables.values():
+            sv.close()

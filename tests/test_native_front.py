@@ -255,3 +255,48 @@ def test_connections_spread_over_the_io_workers(tmp_path):
 
 def test_grpc_message_percent_encoding():
     assert rt.grpc_percent_encode("a b%\né") == "a b%25%0A%C3%A9"
+
+
+def test_oversized_request_resource_exhausted_like_grpcio(tmp_path):
+    """Both front-ends cap the request message (--grpc_max_request_bytes):
+    a larger one is answered RESOURCE_EXHAUSTED with grpcio's wording, and a request within the
+    cap still works. A prefix that lies about its length is covered at the C++ level
+    (csrc/tests/front_stress.cpp oversize phase, under TSAN and ASan in test_sanitizers.py)."""
+    base = _repo(tmp_path)
+    cap = 1 << 20
+    nat = _server(base, "native", grpc_max_request_bytes=cap)
+    py = _server(base, "python", grpc_max_request_bytes=cap)
+    try:
+        big = make_request(np.zeros((4, 299, 299, 3), np.float32)).SerializeToString()   # 4.3 MB > 1 MiB
+        a, b = _call(nat.grpc_port, PREDICT, big), _call(py.grpc_port, PREDICT, big)
+        assert a[0] == b[0] == grpc.StatusCode.RESOURCE_EXHAUSTED.value[0], (a[:2], b[:2])
+        assert a[1] == b[1], (a[1], b[1])
+        small = _u8_req(n=1)[0]                                                        # 268 KB
+        a, b = _call(nat.grpc_port, PREDICT, small), _call(py.grpc_port, PREDICT, small)
+        assert a[0] == 0 and a == b
+        # the native load generator with a raw prefix announcing 2 GiB - 1: refused, nothing buffered
+        liar = b"\0\x7f\xff\xff\xff" + b"x" * 4096
+        r = rt.grpc_load("127.0.0.1", nat.grpc_port, PREDICT, liar, conns=2, streams=64, seconds=0.5,
+                         warm_s=0.0, timeout_s=10.0, raw_frame=True)
+        assert r["error"] == "" and set(r["codes"]) == {8} and r["failed"] > 0, r
+    finally:
+        nat.stop(0)
+        py.stop(0)
+
+
+def test_second_server_on_the_port_fails_unless_shared(tmp_path):
+    """Outside --procs (gpu_index < 0) the native front-end must not silently share a port that
+    another server holds (advisor r5): SO_REUSEPORT stays among its own listeners."""
+    base = _repo(tmp_path)
+    first = _server(base, "native")
+    try:
+        with pytest.raises(Exception):
+            ModelServer(ServerConfig(port=first.grpc_port, rest_api_port=0, model_base_path=str(base),
+                                     device="null", host="127.0.0.1", grpc_frontend="native",
+                                     grpc_io_threads=2)).start(block_until_loaded=True)
+        # a --procs child shares it on purpose
+        shared = rt.GrpcFront("127.0.0.1", first.grpc_port, 1, 1, lambda p, m, d: (12, "x", b"", []),
+                              reuse_port=True)
+        shared.stop()
+    finally:
+        first.stop(0)
