@@ -8,6 +8,7 @@
 #include "kernels/launch.h"
 #include "runtime/engine.h"
 #include "runtime/comm.h"
+#include "runtime/dp_hiploop.h"
 #include "runtime/hip_backend.h"
 
 namespace py = pybind11;
@@ -444,6 +445,64 @@ PYBIND11_MODULE(_C, m) {
         {
           py::gil_scoped_release nogil;
           c = f.run(liveness_s);
+        }
+        return std::make_tuple(c.cmd, c.version, c.seq);
+      }, py::arg("liveness_s") = 30.0);
+  // ---- the same protocol over the HIP loopback platform (runtime/dp_hiploop.h): real engines,
+  // streams and events on one GPU, ranks as threads of this process, device-to-device transport
+  m.def("hiploop_unique_id", []() { return loop::unique_id(); });
+  // module_local: kdl._rt registers the same C++ type (loop::Comm) as LoopComm
+  py::class_<loop::Comm>(m, "HipLoopComm", py::module_local())
+      .def(py::init<const std::string&, int, int>(), py::arg("id"), py::arg("nranks"), py::arg("rank"))
+      .def_property_readonly("rank", &loop::Comm::rank)
+      .def_property_readonly("size", &loop::Comm::size)
+      .def("kill", &loop::Comm::kill)           // this rank stops matching: a dead process
+      .def("abort", &loop::Comm::abort)
+      .def("error", &loop::Comm::error);
+  struct HLLeader {
+    std::unique_ptr<HipLoopLocal> local;
+    std::unique_ptr<HipLoopDpLeader> lead;
+  };
+  struct HLFollower {
+    std::unique_ptr<HipLoopLocal> local;
+    std::unique_ptr<HipLoopDpFollower> f;
+  };
+  py::class_<HLLeader>(m, "HipLoopDpLeader")
+      .def(py::init([](HipExecBackend* be, loop::Comm* sc, loop::Comm* ga, std::vector<int> buckets, double timeout_s,
+                       double ping_s) {
+             auto h = new HLLeader();
+             h->local = std::make_unique<HipLoopLocal>(be);
+             h->lead = std::make_unique<HipLoopDpLeader>(h->local.get(), sc, ga, std::move(buckets), timeout_s, ping_s);
+             return h;
+           }),
+           py::arg("local"), py::arg("scatter"), py::arg("gather"), py::arg("rank_buckets"), py::arg("timeout_s") = 120.0,
+           py::arg("ping_s") = 0.0, py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def("api_ptr", [](const HLLeader& l) { return reinterpret_cast<uintptr_t>(l.lead->api()); })
+      .def_property_readonly("world", [](const HLLeader& l) { return l.lead->world(); })
+      .def_property_readonly("steps", [](const HLLeader& l) { return l.lead->steps(); })
+      .def_property_readonly("broken", [](const HLLeader& l) { return l.lead->broken(); })
+      .def("send_ctrl", [](HLLeader& l, int cmd, int version) {
+        py::gil_scoped_release nogil;
+        return l.lead->send_ctrl(cmd, version);
+      })
+      .def("ping", [](HLLeader& l) {
+        py::gil_scoped_release nogil;
+        return l.lead->ping();
+      });
+  py::class_<HLFollower>(m, "HipLoopDpFollower")
+      .def(py::init([](HipExecBackend* be, loop::Comm* sc, loop::Comm* ga) {
+             auto h = new HLFollower();
+             h->local = std::make_unique<HipLoopLocal>(be);
+             h->f = std::make_unique<HipLoopDpFollower>(h->local.get(), sc, ga);
+             return h;
+           }),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def_property_readonly("steps", [](const HLFollower& f) { return f.f->steps(); })
+      .def("run", [](HLFollower& f, double liveness_s) {
+        DpCtrl c{};
+        {
+          py::gil_scoped_release nogil;
+          c = f.f->run(liveness_s);
         }
         return std::make_tuple(c.cmd, c.version, c.seq);
       }, py::arg("liveness_s") = 30.0);

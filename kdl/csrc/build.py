@@ -44,6 +44,10 @@ def _hipcc() -> str:
 GPU_SOURCES = sorted((HERE / "kernels").glob("*.hip")) + [HERE / "runtime" / "engine.cpp",
                                                          HERE / "runtime" / "hip_backend.cpp",
                                                          HERE / "runtime" / "comm.cpp",
+                                                         # the HIP loopback DP platform (dp_hiploop.h) reuses
+                                                         # the loopback rendezvous of dp_loop.cpp
+                                                         HERE / "runtime" / "dp_loop.cpp",
+                                                         HERE / "runtime" / "dp_hiploop.cpp",
                                                          HERE / "bindings_gpu.cpp"]
 RT_SOURCES = [HERE / "runtime" / n for n in ("batcher.cpp", "executor.cpp", "tfproto.cpp", "sstable.cpp", "dp_loop.cpp",
                                                 "h2.cpp", "grpc_front.cpp", "grpc_load.cpp")] + [

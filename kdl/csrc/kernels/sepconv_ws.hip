@@ -52,26 +52,43 @@ __device__ __forceinline__ void ws_wait_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-// LDS bytes of one workgroup of the configuration (the tile body's layout)
-template <int FM, int FN, int STAGES, int XB>
+// LDS bytes of one workgroup of the configuration (the tile body's layout). ZF: every stage
+// ends in a 256-byte zero block that out-of-map taps read (see ws_tile)
+template <int FM, int FN, int STAGES, int XB, bool ZF = false>
 struct WsSmem {
-  static constexpr int RING = STAGES * (XB + 1) * 1024;
+  static constexpr int RING = STAGES * ((XB + 1) * 1024 + (ZF ? 256 : 0));
   static constexpr int PIPE = RING + 2 * FM * 1024;
   static constexpr int CTILE = 16 * FM * (64 * FN * 2 + 16);
   static constexpr int BYTES = PIPE > CTILE ? PIPE : CTILE;
 };
 
 // One BM x BN output tile of a fused separable conv: the whole body of sepconv_ws_kernel.
-// ABL (timing ablation, id 27, never a candidate; wrong values): 1 = every band glds reads
-// 1 KiB contiguous (8 full lines) instead of 64 pixels x 16 B (64 lines) -- the same loads and
-// bytes, so the counted-vmcnt protocol is untouched, but 8x fewer lines for the TA
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0>
+// ABL (timing ablations, never candidates; wrong values):
+//   1 = every band glds reads 1 KiB contiguous (8 full lines) instead of 64 pixels x 16 B (64
+//       lines) -- the same loads and bytes, so the counted-vmcnt protocol is untouched;
+//   2 = producers skip their band LDS reads (taps from registers); 4 = producers skip the
+//       depthwise MFMAs; 8 = producers skip the A-buffer writes. Each removes LDS / matrix-pipe
+//       work only: every wave still issues and waits for exactly the same global loads.
+// ZF: out-of-map taps (image borders, the 10th tap slot) read a per-stage 256-byte zero block
+// at the 16-byte slot of the same bank as the in-map address would have, instead of one
+// shared zero slot: that slot's bank collided with a live lane of the same ds_read_b128 lane
+// group (2-way conflicts on most dx != 0 taps); and one producer wave, not four, DMAs the
+// depthwise weight entries.
+// PD: the producers read a band three k-steps ahead of its A buffer (two sets of tap registers):
+// in-kernel stamps showed each producer step = the latency of its 16 band reads issued after the
+// barrier (~800 cycles behind the consumers' A reads in the LDS queue) + its depthwise MFMAs;
+// now the reads of band(t+3) complete during steps t and t+1 while the MFMAs of A(t+2) run on
+// registers read a step earlier. Needs a ring one stage deeper (STAGES >= 6).
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0, bool ZF = false,
+          bool PD = false>
 __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, uint8_t* smem) {
   constexpr int NT = 512;
   constexpr int BM = 16 * FM, BN = 64 * FN;
   constexpr int AF = FM;
   constexpr int NSP = 16 * XB, PL = NSP * 16, ZSLOT = NSP - 1;   // band plane: slots, bytes
-  constexpr int STAGE = (XB + 1) * 1024;         // [band XB KiB][depthwise weight entries 1 KiB]
+  // [band XB KiB][depthwise weight entries 1 KiB][ZF: zero block 256 B]
+  constexpr int STAGE = (XB + 1) * 1024 + (ZF ? 256 : 0);
+  constexpr int ZOFF = (XB + 1) * 1024;
   constexpr int WOFF = XB * 1024;
   constexpr int RING = STAGES * STAGE;
   constexpr int ABUF = AF * 1024;
@@ -84,8 +101,9 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   // t+3-STAGES <= t-2; producers read it during step t): everything up to step t-2, so only
   // the LCB + FN loads of step t-1 may still be in flight
   constexpr int WC = LCB + FN;
-  static_assert(FM % 2 == 0 && STAGES >= 5, "layout / pipeline depth");
-  static_assert(SMEM == WsSmem<FM, FN, STAGES, XB>::BYTES, "LDS map");
+  static_assert(FM % 2 == 0 && STAGES >= (PD ? 6 : 5), "layout / pipeline depth");
+  static_assert(SMEM == WsSmem<FM, FN, STAGES, XB, ZF>::BYTES, "LDS map");
+  static_assert(!ZF || (STAGE % 256 == 0 && ZOFF % 256 == 0), "zero block bank alignment");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -209,7 +227,8 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
     load_b(1, b1);
 #pragma unroll
     for (int p = 3; p < STAGES - 1; ++p) issue_band(p, p);
-    ws_wait_barrier<(STAGES - 3) * LCB + 2 * FN>();   // band(0), band(1) landed
+    // band(0), band(1) landed (PD: band(2) as well: the producers' prologue reads three)
+    ws_wait_barrier<(STAGES - (PD ? 4 : 3)) * LCB + 2 * FN>();
     for (int t = 0; t < KTE; t += 2) {
       step(t, b0);
       step(t + 1, b1);
@@ -218,7 +237,13 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
     // ================= producer: dw weights LDS-DMA, depthwise on MFMA
     const int pw = wave - 4;
     const uint8_t* wsrc = (const uint8_t*)a.dwk + lane * 16;
-    auto issue = [&](int t, int slot) { glds16(wsrc + (long)kc(t) * 1024, smem + slot * STAGE + WOFF); };
+    // ZF builds: only producer wave 0 DMAs the step's 1 KiB of depthwise weight entries (the
+    // others used to copy the same bytes to the same LDS bytes: 3 KiB of the ~34 KiB a step
+    // fetches). The others then hold no loads, their counted vmcnt waits are trivially met, and
+    // the barrier after wave 0's wait publishes the entries to them
+    auto issue = [&](int t, int slot) {
+      if (!ZF || pw == 0) glds16(wsrc + (long)kc(t) * 1024, smem + slot * STAGE + WOFF);
+    };
 
     const int g = pw & 1;                        // channel group of all this wave's units
     const int p16 = lane & 15, kb = lane >> 4;
@@ -235,8 +260,13 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
         const int tap = 2 * j + par;
         const int dy = tap / 3 - 1, dx = tap % 3 - 1;
         const bool ok = tap < 9 && (unsigned)(h + dy) < (unsigned)H && (unsigned)(w + dx) < (unsigned)W;
-        const int slot = ok ? (int)(mg + dy * W + dx - P0) : ZSLOT;
-        toff[i][j] = qc * PL + slot * 16;
+        if constexpr (ZF) {
+          const int raw = (int)(mg + dy * W + dx - P0);   // its bank: 4 * raw mod 64 (PL is bank-aligned)
+          toff[i][j] = ok ? qc * PL + raw * 16 : ZOFF + (raw & 15) * 16;
+        } else {
+          const int slot = ok ? (int)(mg + dy * W + dx - P0) : ZSLOT;
+          toff[i][j] = qc * PL + slot * 16;
+        }
       }
     }
     const bool wv = (p16 >> 3) == (kb & 1);
@@ -257,14 +287,22 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
     // over the step instead of piling up behind the barrier with everybody else's) ...
     auto dw_load = [&](int s, u32x4 (&xv)[UPW][5], u32x4& we) {
       const uint8_t* sb = smem + (s % STAGES) * STAGE;
-#pragma unroll
-      for (int i = 0; i < UPW; ++i)
-#pragma unroll
-        for (int j = 0; j < 5; ++j) xv[i][j] = *(const u32x4*)(sb + toff[i][j]);
       we = *(const u32x4*)(sb + went);
+      if constexpr (ABL & 2) {                   // ablation: taps from registers
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+#pragma unroll
+          for (int j = 0; j < 5; ++j) xv[i][j] = we + (uint32_t)(i * 5 + j);
+      } else {
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+#pragma unroll
+          for (int j = 0; j < 5; ++j) xv[i][j] = *(const u32x4*)(sb + toff[i][j]);
+      }
     };
-    // ... and the MFMA part into A buffer abuf; s >= KT (padding step) writes zeros
-    auto dw_mfma = [&](int s, const u32x4 (&xv)[UPW][5], const u32x4 we, int abuf) {
+    // ... and the MFMA part (dacc), written into A buffer abuf by write_a; s >= KT (padding
+    // step) writes zeros
+    auto dw_compute = [&](const u32x4 (&xv)[UPW][5], const u32x4 we, f32x4 (&dacc)[UPW]) {
       s16x8 wf[5];
 #pragma unroll
       for (int j = 0; j < 5; ++j) {
@@ -274,7 +312,6 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
         for (int d = 0; d < 4; ++d) f[d] = __builtin_amdgcn_perm(wd, wd, sel[j & 1][d]);
         wf[j] = __builtin_bit_cast(s16x8, f);
       }
-      f32x4 dacc[UPW];
 #pragma unroll
       for (int i = 0; i < UPW; ++i) dacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -286,33 +323,86 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
 #pragma unroll
             for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
           }
-          dacc[i] = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc[i]);
+          if constexpr (ABL & 4) {               // ablation: no matrix-pipe work
+            dacc[i] += __builtin_bit_cast(f32x4, v) + __builtin_bit_cast(f32x4, wf[j]);
+          } else {
+            dacc[i] = mfma16(wf[j], __builtin_bit_cast(s16x8, v), dacc[i]);
+          }
         }
+    };
+    auto write_a = [&](int s, const f32x4 (&dacc)[UPW], int abuf) {
       const bool live = s < KT;
+      if constexpr (!(ABL & 8)) {
 #pragma unroll
-      for (int i = 0; i < UPW; ++i) {
-        const u32x2 o = {pack_bf16(dacc[i][0], dacc[i][1]), pack_bf16(dacc[i][2], dacc[i][3])};
-        *(u32x2*)(smem + RING + abuf * ABUF + ((pw + 4 * i) >> 1) * 1024 + aoffw) =
-            live ? o : (u32x2){0u, 0u};
+        for (int i = 0; i < UPW; ++i) {
+          const u32x2 o = {pack_bf16(dacc[i][0], dacc[i][1]), pack_bf16(dacc[i][2], dacc[i][3])};
+          *(u32x2*)(smem + RING + abuf * ABUF + ((pw + 4 * i) >> 1) * 1024 + aoffw) =
+              live ? o : (u32x2){0u, 0u};
+        }
+      } else {                                   // ablation: keep the values live, write nothing
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+          asm volatile("" ::"v"(dacc[i][0]), "v"(dacc[i][1]), "v"(dacc[i][2]), "v"(dacc[i][3]));
       }
+    };
+    auto dw_mfma = [&](int s, const u32x4 (&xv)[UPW][5], const u32x4 we, int abuf) {
+      f32x4 dacc[UPW];
+      dw_compute(xv, we, dacc);
+      write_a(s, dacc, abuf);
     };
 
 #pragma unroll
     for (int p = 0; p < STAGES - 1; ++p) issue(p, p);
-    ws_wait_barrier<STAGES - 3>();               // weights of stages 0, 1 (consumers: bands)
-    u32x4 xv[UPW][5], we;
-    dw_load(0, xv, we);
-    dw_mfma(0, xv, we, 0);
-    dw_load(1, xv, we);
-    for (int t = 0; t < KTE; ++t) {
-      ws_wait_barrier<STAGES - 4>();             // stage t+2 landed and published
-      stamp(st0, t);
-      dw_mfma(t + 1, xv, we, (t + 1) & 1);       // inputs read during the previous step
-      dw_load(t + 2, xv, we);                    // consumed next step
-      issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
-      if constexpr (STAMP) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        stamp(st1, t);
+    if constexpr (ZF) {                          // the stages' zero blocks: 16 x 16 B each
+      const int z = pw * 64 + lane;
+      if (z < STAGES * 16) *(u32x4*)(smem + (z >> 4) * STAGE + ZOFF + (z & 15) * 16) = (u32x4){0u, 0u, 0u, 0u};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if constexpr (PD) {
+      ws_wait_barrier<STAGES - 4>();             // weights of stages 0..2 (consumers: bands 0..2)
+      u32x4 xa[UPW][5], xb[UPW][5], wa, wb;
+      f32x4 dacc[UPW];
+      dw_load(0, xa, wa);
+      dw_load(1, xb, wb);
+      dw_mfma(0, xa, wa, 0);                     // A(0)
+      dw_load(2, xa, wa);
+      dw_compute(xb, wb, dacc);                  // A(1), written after barrier 0
+      // step t: write A(t+1); band(t+2) (read in step t-1) is in `cur`; read band(t+3) into
+      // `nxt`; A(t+2) from `cur`. One lgkmcnt(0) per step, right after the two A writes: it
+      // retires the previous step's reads, long landed, never this step's
+      auto pstep = [&](int t, const u32x4 (&cur)[UPW][5], const u32x4& wcur, u32x4 (&nxt)[UPW][5], u32x4& wnxt) {
+        ws_wait_barrier<STAGES - 5>();           // weights of stage t+3 landed and published
+        stamp(st0, t);
+        write_a(t + 1, dacc, (t + 1) & 1);
+        __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0)
+        dw_load(t + 3, nxt, wnxt);
+        dw_compute(cur, wcur, dacc);
+        issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+        if constexpr (STAMP) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          stamp(st1, t);
+        }
+      };
+      for (int t = 0; t < KTE; t += 2) {
+        pstep(t, xa, wa, xb, wb);
+        pstep(t + 1, xb, wb, xa, wa);
+      }
+    } else {
+      ws_wait_barrier<STAGES - 3>();             // weights of stages 0, 1 (consumers: bands)
+      u32x4 xv[UPW][5], we;
+      dw_load(0, xv, we);
+      dw_mfma(0, xv, we, 0);
+      dw_load(1, xv, we);
+      for (int t = 0; t < KTE; ++t) {
+        ws_wait_barrier<STAGES - 4>();           // stage t+2 landed and published
+        stamp(st0, t);
+        dw_mfma(t + 1, xv, we, (t + 1) & 1);     // inputs read during the previous step
+        dw_load(t + 2, xv, we);                  // consumed next step
+        issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+        if constexpr (STAMP) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          stamp(st1, t);
+        }
       }
     }
   }
@@ -354,14 +444,15 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   }
 }
 
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0>
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0, bool ZF = false,
+          bool PD = false>
 __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[WsSmem<FM, FN, STAGES, XB>::BYTES];
+  __shared__ __attribute__((aligned(256))) uint8_t smem[WsSmem<FM, FN, STAGES, XB, ZF>::BYTES];
   constexpr int BM = 16 * FM, BN = 64 * FN;
   const int nN = (a.NF * 16) / BN;
   const int nM = (a.M + BM - 1) / BM;
   const int wg = xcd_remap(blockIdx.x, nM * nN);
-  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, ABL>(a, wg / nN, wg % nN, smem);
+  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, ABL, ZF, PD>(a, wg / nN, wg % nN, smem);
 }
 
 // (FM, FN, STAGES, XB = band KiB): tile BM = 16*FM, BN = 64*FN; LDS = STAGES*(XB+1) KiB + 2FM KiB
@@ -389,13 +480,39 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(24, 6, 6, 5, 11)        \
   X(25, 6, 6, 5, 16)        \
   X(26, 4, 6, 5, 8)          \
-  X(27, 6, 6, 5, 9)
+  X(27, 6, 6, 5, 9)          \
+  X(8, 6, 6, 5, 9)           \
+  X(9, 6, 6, 5, 9)           \
+  X(10, 6, 6, 5, 9)          \
+  X(11, 6, 6, 5, 9)          \
+  X(12, 6, 6, 5, 9)          \
+  X(13, 6, 6, 5, 9)          \
+  X(28, 6, 6, 5, 9)          \
+  X(29, 6, 6, 5, 11)         \
+  X(36, 6, 6, 5, 16)         \
+  X(37, 4, 6, 5, 8)          \
+  X(38, 6, 6, 5, 9)          \
+  X(14, 6, 6, 6, 9)          \
+  X(30, 6, 6, 6, 9)          \
+  X(31, 6, 6, 6, 11)         \
+  X(32, 6, 6, 6, 16)         \
+  X(33, 4, 6, 6, 8)          \
+  X(34, 6, 6, 6, 9)
 
 // id 7: s_memtime stamping variant (tools/stamps.py; never tuned); ids 23-26 = 0, 2, 3, 5
-// walking K from a per-M-tile rotated start
-constexpr bool sepw_stamp(int id) { return id == 7; }
-constexpr bool sepw_krot(int id) { return id >= 23 && id <= 27; }
-constexpr int sepw_abl(int id) { return id == 27 ? 1 : 0; }
+// walking K from a per-M-tile rotated start. Round 6: ids 8-11 = stamped producer ablations
+// (ABL 2, 4, 8, 14) of the rotated 96x384 tile, 12 = its stamped ZF build, 13 = it stamped as is;
+// ids 28, 29, 36, 37 = 23-26 with ZF; 38 = 0 with ZF; 30-33 = 28, 29, 36, 37 with PD (6-stage ring),
+// 34 = 38 with PD, 14 = 30 stamped
+constexpr bool sepw_stamp(int id) { return id == 7 || (id >= 8 && id <= 14); }
+constexpr bool sepw_krot(int id) {
+  return (id >= 8 && id <= 14) || (id >= 23 && id <= 33) || (id >= 36 && id <= 37);
+}
+constexpr int sepw_abl(int id) {
+  return id == 27 ? 1 : id == 8 ? 2 : id == 9 ? 4 : id == 10 ? 8 : id == 11 ? 14 : 0;
+}
+constexpr bool sepw_zf(int id) { return id == 12 || id == 14 || (id >= 28 && id <= 34) || (id >= 36 && id <= 38); }
+constexpr bool sepw_pd(int id) { return id == 14 || (id >= 30 && id <= 34); }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }
 
@@ -430,11 +547,11 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
 #define KDL_SWCASE(id, fm, fn, st, xb)                                                                \
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), true, sepw_abl(id)>), dim3(grid), \
-                         dim3(th), 0, s, a);                                                        \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), true, sepw_abl(id), \
+                                            sepw_zf(id), sepw_pd(id)>), dim3(grid), dim3(th), 0, s, a); \
     else                                                                                            \
-      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), false, sepw_abl(id)>), dim3(grid), \
-                         dim3(th), 0, s, a);                                                        \
+      hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), false, sepw_abl(id), \
+                                            sepw_zf(id), sepw_pd(id)>), dim3(grid), dim3(th), 0, s, a); \
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)
 #undef KDL_SWCASE

@@ -92,6 +92,7 @@ struct Post {
   void* rbuf;
   size_t bytes;
   int state;                                   // 0 pending, 1 delivered, -1 failed
+  CopyFn copy;                                 // receiving post: the byte mover (nullptr: memcpy)
 };
 
 struct World {
@@ -116,6 +117,8 @@ struct World {
         rq.pop_front();
         if (s->bytes != r->bytes) {
           s->state = r->state = -1;            // RCCL would mis-deliver or hang: fail both ends
+        } else if (s->bytes && r->copy) {
+          s->state = r->state = r->copy(r->rbuf, s->sbuf, s->bytes) == 0 ? 1 : -1;
         } else {
           if (s->bytes) std::memcpy(r->rbuf, s->sbuf, s->bytes);
           s->state = r->state = 1;
@@ -255,35 +258,17 @@ int Device::complete(int slot, const float** out, kdl_device_times* t) {
 }  // namespace loop
 
 // ------------------------------------------------------------------------------- platform
-namespace {
-struct LoopOp {
-  bool send;
-  const void* sbuf;
-  void* rbuf;
-  size_t bytes;
-  int peer;
-  loop::Comm* comm;
-  loop::Stream* stream;
-};
-struct LoopGroup {
-  int depth = 0;
-  std::vector<LoopOp> ops;
-};
-thread_local LoopGroup tl_group;
-
-// one stream operation: post every op of the group, then wait (rendezvous) until each was
-// matched, this rank aborted, or its stream was cancelled
-int run_group(const std::vector<LoopOp>& ops) {
-  loop::World* w = ops[0].comm->world();
+namespace loop {
+int rendezvous(const std::vector<Op>& ops, const std::atomic<bool>& cancel, CopyFn copy) {
+  World* w = ops[0].comm->world();
   const int me = ops[0].comm->rank();
-  loop::Stream* st = ops[0].stream;
-  std::vector<loop::Post> posts(ops.size());
+  std::vector<Post> posts(ops.size());
   std::unique_lock<std::mutex> lk(w->mu);
   if (w->aborted[me]) return -1;
   for (size_t i = 0; i < ops.size(); ++i) {
-    const LoopOp& o = ops[i];
+    const Op& o = ops[i];
     if (o.peer < 0 || o.peer >= w->size || o.peer == me) return -1;
-    posts[i] = loop::Post{o.sbuf, o.rbuf, o.bytes, 0};
+    posts[i] = Post{o.sbuf, o.rbuf, o.bytes, 0, copy};
     if (o.send)
       w->sends[{me, o.peer}].push_back(&posts[i]);
     else
@@ -300,7 +285,7 @@ int run_group(const std::vector<LoopOp>& ops) {
     }
     if (failed) rc = -1;
     if (!pending) break;
-    if (failed || w->aborted[me] || st->cancelled().load()) {
+    if (failed || w->aborted[me] || cancel.load()) {
       rc = -1;
       break;
     }
@@ -318,12 +303,30 @@ int run_group(const std::vector<LoopOp>& ops) {
   }
   return rc;
 }
+}  // namespace loop
+
+namespace {
+struct LoopOp {
+  loop::Op op;
+  loop::Stream* stream;
+};
+struct LoopGroup {
+  int depth = 0;
+  std::vector<LoopOp> ops;
+};
+thread_local LoopGroup tl_group;
 
 int submit(std::vector<LoopOp> ops) {
   if (ops.empty()) return 0;
-  for (const auto& o : ops)
-    if (o.comm != ops[0].comm || o.stream != ops[0].stream) return -1;   // one communicator and stream per group
-  ops[0].stream->push([ops] { return run_group(ops); });
+  std::vector<loop::Op> v;
+  for (const auto& o : ops) {
+    if (o.op.comm != ops[0].op.comm || o.stream != ops[0].stream) return -1;   // one communicator and stream per group
+    v.push_back(o.op);
+  }
+  loop::Stream* st = ops[0].stream;
+  // one stream operation: post every op of the group, then wait (rendezvous) until each was
+  // matched, this rank aborted, or its stream was cancelled
+  st->push([v, st] { return loop::rendezvous(v, st->cancelled(), nullptr); });
   return 0;
 }
 
@@ -367,11 +370,11 @@ int LoopPlatform::group_end() {
 }
 
 int LoopPlatform::send(const void* b, size_t n, int peer, Comm& c, Stream s) {
-  return add_op({true, b, nullptr, n, peer, &c, s});
+  return add_op({{true, b, nullptr, n, peer, &c}, s});
 }
 
 int LoopPlatform::recv(void* b, size_t n, int peer, Comm& c, Stream s) {
-  return add_op({false, nullptr, b, n, peer, &c, s});
+  return add_op({{false, nullptr, b, n, peer, &c}, s});
 }
 
 template class DpLeaderT<LoopPlatform>;

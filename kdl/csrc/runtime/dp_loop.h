@@ -95,6 +95,23 @@ class Comm {
 
 std::string unique_id();
 
+// One posted operation of a rendezvous group (one communicator).
+struct Op {
+  bool send;
+  const void* sbuf;
+  void* rbuf;
+  size_t bytes;
+  int peer;
+  Comm* comm;
+};
+// the byte mover of a matched (send, receive) pair, named by the receiving post: 0 = delivered,
+// else both ends fail. nullptr: memcpy (host memory). The HIP loopback platform (dp_hiploop.h)
+// passes a device-to-device copy.
+using CopyFn = int (*)(void* dst, const void* src, size_t n);
+// Post every op, then block until each was matched (and copied), this rank aborted, or `cancel`
+// is set; 0 = all delivered. Used by both loopback platforms from a stream's worker thread.
+int rendezvous(const std::vector<Op>& ops, const std::atomic<bool>& cancel, CopyFn copy);
+
 class Device {
  public:
   Device(int rank, int nslots, size_t item_bytes, int max_batch, int out_cols, std::vector<int> buckets, int version,
