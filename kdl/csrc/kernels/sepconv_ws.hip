@@ -72,15 +72,8 @@ struct WsSmem {
 // ZF: out-of-map taps (image borders, the 10th tap slot) read a per-stage 256-byte zero block
 // at the 16-byte slot of the same bank as the in-map address would have, instead of one
 // shared zero slot: that slot's bank collided with a live lane of the same ds_read_b128 lane
-// group (2-way conflicts on most dx != 0 taps); and one producer wave, not four, DMAs the
-// depthwise weight entries.
-// PD: the producers read a band three k-steps ahead of its A buffer (two sets of tap registers):
-// in-kernel stamps showed each producer step = the latency of its 16 band reads issued after the
-// barrier (~800 cycles behind the consumers' A reads in the LDS queue) + its depthwise MFMAs;
-// now the reads of band(t+3) complete during steps t and t+1 while the MFMAs of A(t+2) run on
-// registers read a step earlier. Needs a ring one stage deeper (STAGES >= 6).
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0, bool ZF = false,
-          bool PD = false>
+// group (2-way conflicts on most dx != 0 taps).
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0, bool ZF = false>
 __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, uint8_t* smem) {
   constexpr int NT = 512;
   constexpr int BM = 16 * FM, BN = 64 * FN;
@@ -101,7 +94,7 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   // t+3-STAGES <= t-2; producers read it during step t): everything up to step t-2, so only
   // the LCB + FN loads of step t-1 may still be in flight
   constexpr int WC = LCB + FN;
-  static_assert(FM % 2 == 0 && STAGES >= (PD ? 6 : 5), "layout / pipeline depth");
+  static_assert(FM % 2 == 0 && STAGES >= 5, "layout / pipeline depth");
   static_assert(SMEM == WsSmem<FM, FN, STAGES, XB, ZF>::BYTES, "LDS map");
   static_assert(!ZF || (STAGE % 256 == 0 && ZOFF % 256 == 0), "zero block bank alignment");
 
@@ -139,6 +132,7 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   // STAMP variants: lane t keeps s_memtime after step t's barrier (st0) and at the end of
   // its work (st1); written out after the loop (no stores inside: they would count in vmcnt)
   unsigned long long st0 = 0, st1 = 0, tstart = 0;
+
   auto stamp = [&](unsigned long long& st, int t) {
     if constexpr (STAMP) {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -227,23 +221,26 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
     load_b(1, b1);
 #pragma unroll
     for (int p = 3; p < STAGES - 1; ++p) issue_band(p, p);
-    // band(0), band(1) landed (PD: band(2) as well: the producers' prologue reads three)
-    ws_wait_barrier<(STAGES - (PD ? 4 : 3)) * LCB + 2 * FN>();
+    ws_wait_barrier<(STAGES - 3) * LCB + 2 * FN>();   // band(0), band(1) landed
     for (int t = 0; t < KTE; t += 2) {
       step(t, b0);
       step(t + 1, b1);
     }
   } else {
     // ================= producer: dw weights LDS-DMA, depthwise on MFMA
+    // STAMP: prologue milestones (setup done, weight DMAs issued, prologue barrier, A(0) written),
+    // producer-side only and stored by the producers: a value held across the consumers' loop
+    // took registers of their in-flight B loads (tools/vmcnt_check.py)
+    unsigned long long pst[4] = {0, 0, 0, 0};
+    auto pstamp = [&](int i) {
+      if constexpr (STAMP) pst[i] = __builtin_amdgcn_s_memtime();
+    };
     const int pw = wave - 4;
     const uint8_t* wsrc = (const uint8_t*)a.dwk + lane * 16;
-    // ZF builds: only producer wave 0 DMAs the step's 1 KiB of depthwise weight entries (the
-    // others used to copy the same bytes to the same LDS bytes: 3 KiB of the ~34 KiB a step
-    // fetches). The others then hold no loads, their counted vmcnt waits are trivially met, and
-    // the barrier after wave 0's wait publishes the entries to them
-    auto issue = [&](int t, int slot) {
-      if (!ZF || pw == 0) glds16(wsrc + (long)kc(t) * 1024, smem + slot * STAGE + WOFF);
-    };
+    // every producer wave DMAs the same 1 KiB of depthwise weight entries: letting only wave 0
+    // load them (round 6) put a branch into the loop body, and hipcc then stopped hoisting the
+    // depthwise MFMAs above the barrier (one basic block each side): +2 us per no-ReLU layer
+    auto issue = [&](int t, int slot) { glds16(wsrc + (long)kc(t) * 1024, smem + slot * STAGE + WOFF); };
 
     const int g = pw & 1;                        // channel group of all this wave's units
     const int p16 = lane & 15, kb = lane >> 4;
@@ -285,10 +282,13 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
 
     // depthwise of stage s in two halves: LDS reads (issued a step ahead, so they are spread
     // over the step instead of piling up behind the barrier with everybody else's) ...
+    // (the weight entries are read LAST: read first, hipcc re-used a register of their destination
+    // as the next tap's address and waited for the read right there -- one LDS round trip inside
+    // every step of the no-ReLU instances, +2 us per layer in the pipelined bench)
     auto dw_load = [&](int s, u32x4 (&xv)[UPW][5], u32x4& we) {
       const uint8_t* sb = smem + (s % STAGES) * STAGE;
-      we = *(const u32x4*)(sb + went);
       if constexpr (ABL & 2) {                   // ablation: taps from registers
+        we = *(const u32x4*)(sb + went);
 #pragma unroll
         for (int i = 0; i < UPW; ++i)
 #pragma unroll
@@ -298,6 +298,7 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
         for (int i = 0; i < UPW; ++i)
 #pragma unroll
           for (int j = 0; j < 5; ++j) xv[i][j] = *(const u32x4*)(sb + toff[i][j]);
+        we = *(const u32x4*)(sb + went);
       }
     };
     // ... and the MFMA part (dacc), written into A buffer abuf by write_a; s >= KT (padding
@@ -351,58 +352,40 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
       write_a(s, dacc, abuf);
     };
 
+    pstamp(0);                                   // setup (tap offsets) done
 #pragma unroll
     for (int p = 0; p < STAGES - 1; ++p) issue(p, p);
+    pstamp(1);
     if constexpr (ZF) {                          // the stages' zero blocks: 16 x 16 B each
       const int z = pw * 64 + lane;
       if (z < STAGES * 16) *(u32x4*)(smem + (z >> 4) * STAGE + ZOFF + (z & 15) * 16) = (u32x4){0u, 0u, 0u, 0u};
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    if constexpr (PD) {
-      ws_wait_barrier<STAGES - 4>();             // weights of stages 0..2 (consumers: bands 0..2)
-      u32x4 xa[UPW][5], xb[UPW][5], wa, wb;
-      f32x4 dacc[UPW];
-      dw_load(0, xa, wa);
-      dw_load(1, xb, wb);
-      dw_mfma(0, xa, wa, 0);                     // A(0)
-      dw_load(2, xa, wa);
-      dw_compute(xb, wb, dacc);                  // A(1), written after barrier 0
-      // step t: write A(t+1); band(t+2) (read in step t-1) is in `cur`; read band(t+3) into
-      // `nxt`; A(t+2) from `cur`. One lgkmcnt(0) per step, right after the two A writes: it
-      // retires the previous step's reads, long landed, never this step's
-      auto pstep = [&](int t, const u32x4 (&cur)[UPW][5], const u32x4& wcur, u32x4 (&nxt)[UPW][5], u32x4& wnxt) {
-        ws_wait_barrier<STAGES - 5>();           // weights of stage t+3 landed and published
-        stamp(st0, t);
-        write_a(t + 1, dacc, (t + 1) & 1);
-        __builtin_amdgcn_s_waitcnt(0xc07f);      // lgkmcnt(0)
-        dw_load(t + 3, nxt, wnxt);
-        dw_compute(cur, wcur, dacc);
-        issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
-        if constexpr (STAMP) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          stamp(st1, t);
-        }
-      };
-      for (int t = 0; t < KTE; t += 2) {
-        pstep(t, xa, wa, xb, wb);
-        pstep(t + 1, xb, wb, xa, wa);
+    ws_wait_barrier<STAGES - 3>();             // weights of stages 0, 1 (consumers: bands)
+    pstamp(2);
+    u32x4 xv[UPW][5], we;
+    dw_load(0, xv, we);
+    dw_mfma(0, xv, we, 0);
+    dw_load(1, xv, we);
+    if constexpr (STAMP) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pstamp(3);                               // A(0) written, band(1) read
+    }
+    for (int t = 0; t < KTE; ++t) {
+      ws_wait_barrier<STAGES - 4>();           // stage t+2 landed and published
+      stamp(st0, t);
+      dw_mfma(t + 1, xv, we, (t + 1) & 1);     // inputs read during the previous step
+      dw_load(t + 2, xv, we);                  // consumed next step
+      issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      if constexpr (STAMP) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stamp(st1, t);
       }
-    } else {
-      ws_wait_barrier<STAGES - 3>();             // weights of stages 0, 1 (consumers: bands)
-      u32x4 xv[UPW][5], we;
-      dw_load(0, xv, we);
-      dw_mfma(0, xv, we, 0);
-      dw_load(1, xv, we);
-      for (int t = 0; t < KTE; ++t) {
-        ws_wait_barrier<STAGES - 4>();           // stage t+2 landed and published
-        stamp(st0, t);
-        dw_mfma(t + 1, xv, we, (t + 1) & 1);     // inputs read during the previous step
-        dw_load(t + 2, xv, we);                  // consumed next step
-        issue(t + STAGES - 1, (t + STAGES - 1) % STAGES);
-        if constexpr (STAMP) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          stamp(st1, t);
-        }
+    }
+    if constexpr (STAMP) {
+      if (a.stamps && blockIdx.x < 64 && lane == 0) {
+        unsigned long long* o = a.stamps + ((long)blockIdx.x * 8 + wave) * 130;
+        for (int i = 0; i < 4; ++i) o[120 + i] = pst[i] ? pst[i] - tstart : 0;
       }
     }
   }
@@ -444,15 +427,14 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
   }
 }
 
-template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0, bool ZF = false,
-          bool PD = false>
+template <int FM, int FN, int STAGES, int XB, bool STAMP, bool KROT, bool RELU, int ABL = 0, bool ZF = false>
 __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   __shared__ __attribute__((aligned(256))) uint8_t smem[WsSmem<FM, FN, STAGES, XB, ZF>::BYTES];
   constexpr int BM = 16 * FM, BN = 64 * FN;
   const int nN = (a.NF * 16) / BN;
   const int nM = (a.M + BM - 1) / BM;
   const int wg = xcd_remap(blockIdx.x, nM * nN);
-  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, ABL, ZF, PD>(a, wg / nN, wg % nN, smem);
+  ws_tile<FM, FN, STAGES, XB, STAMP, KROT, RELU, ABL, ZF>(a, wg / nN, wg % nN, smem);
 }
 
 // (FM, FN, STAGES, XB = band KiB): tile BM = 16*FM, BN = 64*FN; LDS = STAGES*(XB+1) KiB + 2FM KiB
@@ -491,28 +473,20 @@ __global__ __launch_bounds__(512) void sepconv_ws_kernel(ConvGemmArgs a) {
   X(29, 6, 6, 5, 11)         \
   X(36, 6, 6, 5, 16)         \
   X(37, 4, 6, 5, 8)          \
-  X(38, 6, 6, 5, 9)          \
-  X(14, 6, 6, 6, 9)          \
-  X(30, 6, 6, 6, 9)          \
-  X(31, 6, 6, 6, 11)         \
-  X(32, 6, 6, 6, 16)         \
-  X(33, 4, 6, 6, 8)          \
-  X(34, 6, 6, 6, 9)
+  X(38, 6, 6, 5, 9)
 
 // id 7: s_memtime stamping variant (tools/stamps.py; never tuned); ids 23-26 = 0, 2, 3, 5
 // walking K from a per-M-tile rotated start. Round 6: ids 8-11 = stamped producer ablations
 // (ABL 2, 4, 8, 14) of the rotated 96x384 tile, 12 = its stamped ZF build, 13 = it stamped as is;
-// ids 28, 29, 36, 37 = 23-26 with ZF; 38 = 0 with ZF; 30-33 = 28, 29, 36, 37 with PD (6-stage ring),
-// 34 = 38 with PD, 14 = 30 stamped
-constexpr bool sepw_stamp(int id) { return id == 7 || (id >= 8 && id <= 14); }
-constexpr bool sepw_krot(int id) {
-  return (id >= 8 && id <= 14) || (id >= 23 && id <= 33) || (id >= 36 && id <= 37);
-}
+// ids 28, 29, 36, 37 = 23-26 with ZF; 38 = 0 with ZF. (Round 6 also measured a producer read-ahead
+// by three k-steps over a 6-stage ring, ids 30-34: slower isolated and in the pipelined bench,
+// hipcc hoisting the next step's MFMAs across the barrier; removed.)
+constexpr bool sepw_stamp(int id) { return id == 7 || (id >= 8 && id <= 13); }
+constexpr bool sepw_krot(int id) { return (id >= 8 && id <= 13) || (id >= 23 && id <= 29) || (id >= 36 && id <= 37); }
 constexpr int sepw_abl(int id) {
   return id == 27 ? 1 : id == 8 ? 2 : id == 9 ? 4 : id == 10 ? 8 : id == 11 ? 14 : 0;
 }
-constexpr bool sepw_zf(int id) { return id == 12 || id == 14 || (id >= 28 && id <= 34) || (id >= 36 && id <= 38); }
-constexpr bool sepw_pd(int id) { return id == 14 || (id >= 30 && id <= 34); }
+constexpr bool sepw_zf(int id) { return id == 12 || id == 28 || id == 29 || (id >= 36 && id <= 38); }
 
 static int sepw_fits_xb(int BM, int W, int xb) { return BM + 2 * W + 3 <= 16 * xb; }
 
@@ -548,10 +522,10 @@ hipError_t sepconv_ws(int cfg, const ConvGemmArgs& args, hipStream_t s) {
   case id:                                                                                          \
     if (a.relu_in)                                                                                  \
       hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), true, sepw_abl(id), \
-                                            sepw_zf(id), sepw_pd(id)>), dim3(grid), dim3(th), 0, s, a); \
+                                            sepw_zf(id)>), dim3(grid), dim3(th), 0, s, a);           \
     else                                                                                            \
       hipLaunchKernelGGL((sepconv_ws_kernel<fm, fn, st, xb, sepw_stamp(id), sepw_krot(id), false, sepw_abl(id), \
-                                            sepw_zf(id), sepw_pd(id)>), dim3(grid), dim3(th), 0, s, a); \
+                                            sepw_zf(id)>), dim3(grid), dim3(th), 0, s, a);           \
     break;
     KDL_SEPW_CONFIGS(KDL_SWCASE)
 #undef KDL_SWCASE

@@ -53,11 +53,8 @@ CONFIGS = {0: (2, 2, 2, 2), 1: (4, 2, 2, 2), 2: (2, 4, 2, 2), 3: (4, 4, 2, 2), 4
            128: (6, 6, 1, 4), 129: (6, 6, 1, 4), 130: (6, 6, 1, 4), 131: (6, 6, 1, 4), 132: (6, 6, 1, 4),
            133: (6, 6, 1, 4), 148: (6, 6, 1, 4), 149: (6, 6, 1, 4), 156: (6, 6, 1, 4), 157: (4, 6, 1, 4),
            158: (6, 6, 1, 4),
-           # 150-153 = 148, 149, 156, 157 with the producers reading three k-steps ahead (PD, 6-stage
-           # ring), 154 = 158 with PD, 134 = 150 stamped
-           150: (6, 6, 1, 4), 151: (6, 6, 1, 4), 152: (6, 6, 1, 4), 153: (4, 6, 1, 4), 154: (6, 6, 1, 4),
-           134: (6, 6, 1, 4),
-           # (150-155 held round 4's wide-tile variant until it measured 1.5-2.2x slower: profiles/sepconv_wide_r4.txt)
+           # 150-155: round 4's wide-tile variant and round 6's producer read-ahead, both measured slower and
+           # removed (profiles/sepconv_wide_r4.txt, profiles/middle_flow_r6.txt)
            # fused separable conv over 2-D TH x TW pixel tiles (sepconv_2d.hip, KDL_S2D_CONFIGS)
            160: (3, 2, 2, 4), 161: (4, 2, 2, 4), 162: (2, 2, 2, 4), 163: (3, 4, 2, 4), 164: (4, 4, 2, 4),
            165: (4, 2, 2, 4), 166: (2, 4, 2, 4), 167: (3, 2, 2, 4), 168: (4, 1, 2, 4), 169: (2, 1, 4, 2),
@@ -86,8 +83,7 @@ S2D_MIN_W = 64    # 16-pixel tile rows waste too much of a narrower map (37 -> 4
 SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
            135: 15, 136: 11, 137: 15, 140: 8, 141: 8, 142: 8,
            143: 9, 144: 11, 145: 16, 146: 8, 147: 9,
-           128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 148: 9, 149: 11, 156: 16, 157: 8, 158: 9,
-           150: 9, 151: 11, 152: 16, 153: 8, 154: 9, 134: 9}
+           128: 9, 129: 9, 130: 9, 131: 9, 132: 9, 133: 9, 148: 9, 149: 11, 156: 16, 157: 8, 158: 9}
 # ids 1000..1999 were the hipBLASLt node (rounds 3-4); retired in round 5 -- every GEMM of the
 # product is hand-written (the vendor library stays a measuring stick: tools/gemm_vs_vendor.py)
 # ids >= SPLITK_BASE: an LDS-DMA GEMM config (16..63) with K split over ksplit workgroups per tile
@@ -102,7 +98,7 @@ STREAM_NT = 3001
 STREAM_IDS = (STREAM_BASE, STREAM_NT)
 STREAM_SHAPES = frozenset([(1, 2), (2, 2), (1, 12), (6, 4), (2, 18), (9, 4), (9, 6), (3, 30), (15, 6)])
 # never autotune candidates: the ws stamping build and band ablation
-ABLATION_IDS = frozenset([127, 147, 128, 129, 130, 131, 132, 133, 134])
+ABLATION_IDS = frozenset([127, 147, 128, 129, 130, 131, 132, 133])
 
 
 def s2dp_smem(cfg: int, K: int) -> int:

@@ -19,6 +19,7 @@ from kdl.ops.conv import MODE_DW, MODE_PW, MODE_CONV, Geometry, cfg_tile
 SHAPES = {
     # name: (mode, cin, n, H, stride)
     "mid_sep": (MODE_DW, 728, 728, 19, 1),
+    "mid_sep_nr": (MODE_DW, 728, 728, 19, 1),   # without the pre-ReLU (sepconv2 / 3 of a middle block)
     "mid_pw": (MODE_PW, 728, 728, 19, 1),
     "b2_sep2": (MODE_DW, 128, 128, 147, 1),
     "b2_sep1": (MODE_DW, 64, 128, 147, 1),
@@ -62,7 +63,7 @@ def main():
     s = torch.cuda.current_stream()
     for name in a.shapes.split(","):
         mode, cin, n, H, stride = SHAPES[name]
-        lay = _layer(mode, cin, n, gen, stride=stride, relu_in=mode == MODE_DW)
+        lay = _layer(mode, cin, n, gen, stride=stride, relu_in=mode == MODE_DW and not name.endswith("_nr"))
         B = a.batch
         if mode == MODE_CONV:
             g = Geometry(B, H, H, H - 2, H - 2)

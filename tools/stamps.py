@@ -73,6 +73,10 @@ def main():
         med = statistics.median
         print(f"  {role}: step {med(per):7.0f}  work {med(work):7.0f}  wait {med(wait):7.0f}  "
               f"prologue {med(pro):7.0f}  loop-end->end {med(epi):7.0f}  total {med(tot):8.0f} cycles")
+        # prologue milestones (cycles after kernel entry): setup done, loads issued, prologue barrier,
+        # (producers) A(0) written
+        ms = [[s[b, w, 120 + i].item() for b in range(64) for w in waves] for i in range(4)]
+        print(f"    prologue milestones: " + "  ".join(f"p{i} {med(m):6.0f}" for i, m in enumerate(ms) if any(m)))
 
 
 if __name__ == "__main__":
