@@ -123,9 +123,9 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--settle", type=float, default=0.5,
-                    help="minimum seconds of untimed graph replays before the warmup steps (GPU clock ramp)")
+                    help="minimum seconds of untimed pipelined steps before the warmup steps (GPU clock ramp)")
     ap.add_argument("--settle-max", type=float, default=3.0,
-                    help="untimed replays continue past --settle until two consecutive 10-replay chunks "
+                    help="untimed steps continue past --settle until two consecutive 10-step chunks "
                          "agree within 1 %% (a stable replay time), for at most this many seconds")
     ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
     ap.add_argument("--model", default="xception",
@@ -399,28 +399,38 @@ def main(argv=None) -> int:
     # setup (not a warmup step): capture both slots' graphs and let the clocks ramp
     for j in range(NS):
         eng.program(B, use_graph, j)
-    # settle: replay until the replay time is stable (clock ramp on a fresh lease), at least
-    # --settle and at most --settle-max seconds; untimed, before the warmup steps
+    # settle: run the pipelined step itself (untimed, before the warmup steps) until its time is
+    # stable -- at least --settle and at most --settle-max seconds. Serial replays were used until
+    # round 6, but the pipelined regime kept speeding up for ~60 steps after them (20 steps after
+    # 5 warmup steps read 1.28 ms/step, after 60 warmup steps 1.254: profiles/bench_settle_r6.txt).
+    # Ranks agree on every chunk (a step may hold collectives), so all run the same count.
+    for i in range(a.depth):
+        ingress(i)
+    nxt = 0
     t_start = time.perf_counter()
     chunk_ms: list[float] = []
     while True:
         c0 = time.perf_counter()
         for _ in range(10):
-            eng.launch(B, s, capture=use_graph)
+            step(nxt)
+            nxt += 1
         torch.cuda.synchronize()
         chunk_ms.append((time.perf_counter() - c0) * 1e3)
         spent = time.perf_counter() - t_start
         stable = len(chunk_ms) >= 3 and abs(chunk_ms[-1] - chunk_ms[-2]) <= 0.01 * chunk_ms[-2]
-        if spent >= a.settle_max or (spent >= a.settle and stable):
+        more = not (spent >= a.settle_max or (spent >= a.settle and stable))
+        if dist_on:
+            t = torch.tensor([int(more)], device=cdev, dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            more = bool(t.item())
+        if not more:
             break
     settle_s = time.perf_counter() - t_start
-    if rank == 0:   # clock-ramp trajectory of the untimed replays (fresh-lease diagnosis, stderr only)
-        print("settle chunks (10 replays, ms): " + " ".join(f"{c:.2f}" for c in chunk_ms), file=sys.stderr)
+    if rank == 0:   # settle trajectory of the untimed pipelined steps (fresh-lease diagnosis, stderr only)
+        print("settle chunks (10 pipelined steps, ms): " + " ".join(f"{c:.2f}" for c in chunk_ms), file=sys.stderr)
     if dist_on:
         dist.barrier()
-    for i in range(a.depth):
-        ingress(i)
-    for i in range(a.warmup):
+    for i in range(nxt, nxt + a.warmup):
         step(i)
     torch.cuda.synchronize()
     if dist_on:
@@ -429,7 +439,7 @@ def main(argv=None) -> int:
 
     tt[:] = [0.0, 0.0, 0.0]
     t0 = time.perf_counter()
-    for i in range(a.warmup, total):
+    for i in range(nxt + a.warmup, nxt + total):
         step(i)
     t_issue = time.perf_counter() - t0
     torch.cuda.synchronize()

@@ -27,9 +27,15 @@ SHAPES = {
     "b3_sep2": (MODE_DW, 256, 256, 74, 1),
     "b4_sep2": (MODE_DW, 728, 728, 37, 1),
     "b14_sep2": (MODE_DW, 1536, 2048, 10, 1),
+    "b14_sep1_nr": (MODE_DW, 1024, 1536, 10, 1),   # block14_sepconv1 (no ReLU before it)
     "stem2": (MODE_CONV, 32, 64, 149, 1),
     "b4_res": (MODE_PW, 256, 728, 37, 2),      # block4 residual 1x1/2 (conv2d_2)
     "b13_res": (MODE_PW, 728, 1024, 19, 2),    # block13 residual 1x1/2 (conv2d_3)
+    # the split lowering's pointwise GEMMs of blocks 4 / 13 / 14 (after their depthwise kernels)
+    "b4_pw1": (MODE_PW, 256, 728, 37, 1),
+    "b4_pw2": (MODE_PW, 728, 728, 37, 1),
+    "b13_pw2": (MODE_PW, 728, 1024, 19, 1),
+    "b14_pw2": (MODE_PW, 1536, 2048, 10, 1),
     # ablations of the middle-flow GEMM: K x2 / x0.5, M x2 (via --batch)
     "mid_pw_k2": (MODE_PW, 1456, 728, 19, 1),
     "mid_pw_kh": (MODE_PW, 352, 728, 19, 1),
@@ -54,6 +60,8 @@ def main():
     ap.add_argument("--top", type=int, default=6)
     ap.add_argument("--cfgs", default=None, help="comma list of (fused) config ids to time instead of all variants; "
                                                   "s<id> for the split lowering")
+    ap.add_argument("--vendor", action="store_true",
+                    help="MODE_PW shapes: also time torch.matmul bf16 (hipBLASLt; GEMM only, no bias / ReLU)")
     a = ap.parse_args()
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
@@ -93,6 +101,22 @@ def main():
                 e1.synchronize()
                 times[(split, cfg)].append(e0.elapsed_time(e1) / a.iters * 1e3)
         print(f"== {name}: M={g.M} K={lay.K} N={n} ({macs / 1e9:.2f} GMAC)")
+        if a.vendor and mode == MODE_PW:
+            xa = torch.randn((g.M, cin), dtype=torch.bfloat16, device="cuda")
+            wb = torch.randn((cin, n), dtype=torch.bfloat16, device="cuda")
+            out = torch.empty((g.M, n), dtype=torch.bfloat16, device="cuda")
+            vt = []
+            for _ in range(a.rounds):
+                torch.matmul(xa, wb, out=out)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    torch.matmul(xa, wb, out=out)
+                e1.record()
+                e1.synchronize()
+                vt.append(e0.elapsed_time(e1) / a.iters * 1e3)
+            t = statistics.median(vt)
+            print(f"   hipBLASLt (torch.matmul bf16, GEMM only): {t:8.1f} us  {2 * macs / t / 1e6:7.1f} TF/s")
         for (split, cfg), ts in sorted(times.items(), key=lambda kv: min(kv[1]))[:a.top]:
             t = statistics.median(ts)
             print(f"   {'split' if split else 'fused'} cfg {cfg:2d} tile {cfg_tile(cfg)}: {t:8.1f} us  "
