@@ -135,7 +135,14 @@ def main(argv=None) -> int:
                          "slots) to measure what ingress overlap costs; never a reported number")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--depth", type=int, default=3,
-                    help="ingress prefetch distance in batches (input slots = depth + 1)")
+                    help="ingress prefetch distance in batches (input slots = depth + 1 + slack)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="DIAGNOSTIC: timing events around every pipeline stage of the timed steps; prints per-stage "
+                         "busy / overlap / idle to stderr (the events sit inside the timed window)")
+    ap.add_argument("--slack", type=int, default=0,
+                    help="extra input slots: the host's ingress of batch i+depth waits for batch i-1-slack "
+                         "to finish instead of batch i-1, so the next batch is already queued on the GPU "
+                         "when a batch retires (0: the pre-round-6 behaviour)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="split each GPU's batch into this many concurrent hipGraph lanes "
                          "(kdl/engine/lanes.py; default 2 when the batch is even)")
@@ -254,7 +261,7 @@ def main(argv=None) -> int:
     # one pinned host batch per slot (a server's requests land in distinct staging buffers;
     # re-issuing copies from ONE pinned buffer while its previous copy is still queued
     # blocked hipMemcpyAsync on the host for ~0.6 ms per step)
-    NS = a.depth + 1
+    NS = a.depth + 1 + a.slack
     hosts = ([torch.randint(0, 256, (n_host, S, S, 3), generator=g, dtype=torch.uint8).pin_memory()
               for _ in range(NS)] if has_host else None)
     # NS engine slots (input + logits buffer, each with its own captured graph): batch
@@ -438,6 +445,8 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
 
     tt[:] = [0.0, 0.0, 0.0]
+    if a.timeline and a.stages:
+        eng.trace = []
     t0 = time.perf_counter()
     for i in range(nxt + a.warmup, nxt + total):
         step(i)
@@ -447,6 +456,9 @@ def main(argv=None) -> int:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if a.timeline and a.stages and rank == 0:
+        _print_timeline(eng.trace, len(eng.ranges))
+        eng.trace = None
     if dist_on:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -512,6 +524,30 @@ def main(argv=None) -> int:
     if dist_on:
         dist.destroy_process_group()
     return 0
+
+
+def _print_timeline(trace: list, K: int) -> None:
+    """--timeline: per-stage busy time, the time both stages ran at once and each stream's idle
+    time between its consecutive stage runs, from the timing events around every stage launch."""
+    ref = trace[0][2]
+    iv = [(k, ref.elapsed_time(e0), ref.elapsed_time(e1)) for _, k, e0, e1 in trace]
+    span = max(e for _, _, e in iv) - min(s for _, s, _ in iv)
+    n = len(iv) // K
+    out = [f"timeline: {n} batches, {span / n * 1e3:.1f} us per batch"]
+    for k in range(K):
+        mine = sorted((s, e) for kk, s, e in iv if kk == k)
+        busy = sum(e - s for s, e in mine)
+        idle = sum(max(0.0, b[0] - a[1]) for a, b in zip(mine, mine[1:]))
+        out.append(f"  stage {k + 1}: run {busy / n * 1e3:7.1f} us/batch, idle between runs {idle / max(1, n - 1) * 1e3:7.1f} us")
+    ev = sorted([(s, 1) for _, s, _ in iv] + [(e, -1) for _, _, e in iv])
+    cnt, last, both = 0, None, 0.0
+    for t, d in ev:
+        if last is not None and cnt >= 2:
+            both += t - last
+        cnt += d
+        last = t
+    out.append(f"  two stages at once: {both / n * 1e3:.1f} us/batch")
+    print("\n".join(out), file=sys.stderr)
 
 
 def dry_run(a, rank: int, local: int, world: int) -> int:

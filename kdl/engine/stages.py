@@ -186,6 +186,7 @@ class StagePipe:
         for e in self.done[0] + self.done[1]:     # "done" before the first batch
             e.record(self.streams[0])
         self._n = 0                               # batches issued (parity of the next one)
+        self.trace: list | None = None            # [(batch, stage, start event, end event)] when a list
         engine.add_input_slots(1)
         self.inputs, self.outputs = engine.inputs, engine.outputs
         self.inp, self.logits = engine.inputs[0], engine.outputs[0]
@@ -256,7 +257,13 @@ class StagePipe:
                 st.wait_event(ev[k - 1])
             if self.wait_for[k] > k:
                 st.wait_event(ev[self.wait_for[k]])   # recorded by batch i-2: its reader is done
+            if self.trace is not None:            # diagnostic timeline (bench.py --timeline)
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record(st)
             prog.launch(int(st.cuda_stream))
+            if self.trace is not None:
+                t1.record(st)
+                self.trace.append((self._n - 1, k, t0, t1))
             ev[k].record(st)
         done[0].record(self.streams[-1])
 
