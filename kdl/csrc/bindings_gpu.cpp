@@ -49,6 +49,8 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.ksplit = I(d, "ksplit");
   a.ws = P<float>(d, "ws");
   a.cnt = P<int>(d, "cnt");
+  a.ascale = P<const float>(d, "ascale");
+  a.ascale_ld = I(d, "ascale_ld");
   return a;
 }
 float F(const py::dict& d, const char* k, float def) {

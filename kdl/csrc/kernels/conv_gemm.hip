@@ -291,6 +291,9 @@ static hipError_t launch_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
 
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (a.K % 32 != 0 || a.M <= 0 || a.dt < 0 || a.dt > 1) return hipErrorInvalidValue;
+  // A-operand channel scales: the LDS-DMA pipelined and streaming GEMMs only (any other kernel
+  // would ignore them)
+  if (a.ascale && cfg < STREAM_CFG_BASE && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE)) return hipErrorInvalidValue;
   if (cfg >= STREAM_CFG_BASE)
     return mode == MODE_PW && cfg <= STREAM_CFG_BASE + 1 ? gemm_stream(a, cfg == STREAM_CFG_BASE + 1, s)
                                                          : hipErrorInvalidValue;

@@ -21,6 +21,17 @@
 
 namespace kdl {
 
+// ASC: one A fragment (8 consecutive k of one row, bf16) times its 8 channel scales (fp32), back to bf16
+__device__ __forceinline__ s16x8 pipe_ascale8(const s16x8 v, const f32x4 s0, const f32x4 s1) {
+  const u32x4 u = __builtin_bit_cast(u32x4, v);
+  u32x4 o;
+  o[0] = pack_bf16(bf_lo(u[0]) * s0[0], bf_hi(u[0]) * s0[1]);
+  o[1] = pack_bf16(bf_lo(u[1]) * s0[2], bf_hi(u[1]) * s0[3]);
+  o[2] = pack_bf16(bf_lo(u[2]) * s1[0], bf_hi(u[2]) * s1[1]);
+  o[3] = pack_bf16(bf_lo(u[3]) * s1[2], bf_hi(u[3]) * s1[3]);
+  return __builtin_bit_cast(s16x8, o);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
@@ -28,14 +39,19 @@ __device__ __forceinline__ void wait_vm_barrier() {
 
 // DT: element type (common.h Elt): 0 bf16, 1 fp16. (Round 2's timing ablations of this
 // kernel -- no MFMA / no DMA / no stores / contiguous A -- are in profiles/kernel_ablations_r2.txt.)
-template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int DT = 0>
+// ASC: per-image channel scales on A (ConvGemmArgs.ascale; MODE_PW bf16): each stage gets one more
+// 1 KiB DMA slot holding the k-step's 32 scales of the tile's image (128 bytes, repeated), read as
+// 2 broadcast ds_read_b128 per lane and applied to the A fragments in registers before the MFMAs.
+template <int MODE, int FM, int FN, int WGM, int WGN, int STAGES, int KSUB, int DT = 0, bool ASC = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs a) {
   using E = Elt<DT>;
+  static_assert(!ASC || (MODE == 0 && DT == 0), "A-operand scales: bf16 pointwise only");
   constexpr int NW = WGM * WGN;
   constexpr int BM = 16 * FM * WGM;
   constexpr int BN = 16 * FN * WGN;
   constexpr int AF = BM / 16, BF = BN / 16;
-  constexpr int FR = AF + BF;                 // 1 KiB fragments per stage
+  constexpr int FRD = AF + BF;                // operand fragments per k-step
+  constexpr int FR = FRD + (ASC ? 1 : 0);     // 1 KiB DMA slots per k-step (+ the scales)
   // LDS-DMA instructions per wave per stage. When FR does not split evenly, the
   // surplus slots re-issue the last fragment (identical bytes to the identical
   // LDS slot), so every wave issues exactly L and one counted vmcnt fits all.
@@ -52,9 +68,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   const int wm = wave / WGN, wn = wave % WGN;
   const int nN = (a.NF * 16) / BN;
   const int OHW = a.OH * a.OW;
-  // per-image weights (a.wimg): M tiles are cut per image so a tile has one weight set
-  const int mpi = a.wimg ? (OHW + BM - 1) / BM : 0;
-  const int nM = a.wimg ? a.B * mpi : (a.M + BM - 1) / BM;
+  // per-image weights (a.wimg) or A scales (ASC): M tiles are cut per image so a tile has one
+  // weight set / one scale vector
+  const bool per_img = a.wimg || ASC;
+  const int mpi = per_img ? (OHW + BM - 1) / BM : 0;
+  const int nM = per_img ? a.B * mpi : (a.M + BM - 1) / BM;
   // split-K: consecutive logical ids are the splits of one tile (same XCD: their partials meet in L2)
   const int S = a.ksplit > 1 ? a.ksplit : 1;
   const int tiles = nM * nN;
@@ -63,8 +81,9 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   const int mi = tile / nN, ni = tile % nN;
   int m0 = mi * BM, mend = a.M;
   long wofs = 0;
-  if (a.wimg) {
-    const int bi = mi / mpi;
+  int bi = 0;
+  if (per_img) {
+    bi = mi / mpi;
     m0 = bi * OHW + (mi - bi * mpi) * BM;
     mend = (bi + 1) * OHW;
     wofs = (long)bi * a.wimg;
@@ -86,9 +105,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       const long pix = ((long)b * a.H + (long)oh * a.stride) * a.W + (long)ow * a.stride;
       src[i] = pix * a.ldx + 8 * (lane >> 4);
-    } else {
+    } else if (f < FRD) {
       const int nf = n0 / 16 + (f - AF);
       src[i] = wofs + ((long)nf * (a.K >> 5)) * 512 + lane * 8;
+    } else {                                  // ASC: 8 lanes x 16 B = the k-step's 32 scales, repeated
+      src[i] = (long)bi * a.ascale_ld + (lane & 7) * 4;
     }
   }
 
@@ -116,7 +137,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       for (int i = 0; i < L; ++i) {
         const int f = min(wave + i * NW, FR - 1);
         if (f < AF) glds16(a.x + src[i] + koff_a, base + f * 1024);
-        else glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
+        else if (!ASC || f < FRD) glds16(a.wp + src[i] + (long)k32 * 512, base + f * 1024);
+        else glds16(a.ascale + src[i] + (long)k32 * 32, base + f * 1024);
       }
     }
   };
@@ -147,6 +169,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       for (int i = 0; i < FM; ++i) af[i] = *(const s16x8*)(st + (wm * FM + i) * 1024);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bf[j] = *(const s16x8*)(st + (AF + wn * FN + j) * 1024);
+      if constexpr (ASC) {                    // this lane's 8 k (8 * (lane >> 4) ..): 32 bytes of scales
+        const uint8_t* sc = st - lane * 16 + FRD * 1024 + (lane >> 4) * 32;
+        const f32x4 s0 = *(const f32x4*)sc, s1 = *(const f32x4*)(sc + 16);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = pipe_ascale8(af[i], s0, s1);
+      }
       // raise this wave's issue priority while it streams MFMAs (guide §5 T-setprio:
       // the other waves' glds issue / barrier arrival no longer interleave into the
       // MFMA run)
@@ -274,24 +302,26 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
 // 6304 rows) they fill 256 CUs in whole waves: out_proj / mlp.3 (N 768) 160x128 -> 240
 // tiles; QKV (N 2304) 160x192 -> 480; mlp.0 (N 3072) 160x256 -> 480 (vs 192x192: 396 / 528)
 
-template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int DT = 0>
+template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int DT = 0, bool ASC = false>
 static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
-  if (a.wimg && (a.M != a.B * a.OH * a.OW || a.B <= 0)) return hipErrorInvalidValue;
-  const int nM = a.wimg ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
+  const bool per_img = a.wimg || ASC;
+  if (per_img && (a.M != a.B * a.OH * a.OW || a.B <= 0)) return hipErrorInvalidValue;
+  if (ASC && (!a.ascale || a.ascale_ld < a.K || a.ascale_ld % 4 != 0)) return hipErrorInvalidValue;
+  const int nM = per_img ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
   const int S = a.ksplit > 1 ? a.ksplit : 1;
-  if (S > 1 && ((a.K / 32) % S != 0 || !a.ws || !a.cnt || a.wimg || S > 16)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT>), dim3(nM * nN * S),
+  if (S > 1 && ((a.K / 32) % S != 0 || !a.ws || !a.cnt || per_img || S > 16)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_pipe_kernel<MODE, FM, FN, WGM, WGN, ST, KS, DT, ASC>), dim3(nM * nN * S),
                      dim3(64 * WGM * WGN), 0, s, a);
   return hipGetLastError();
 }
 
-template <int MODE, int DT>
+template <int MODE, int DT, bool ASC = false>
 static hipError_t launch_pipe_mode(int cfg, const ConvGemmArgs& a, hipStream_t s) {
   switch (cfg) {
 #define KDL_PCASE(id, fm, fn, wgm, wgn, st, ks) \
-  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, DT>(a, s);
+  case id: return launch_pipe_cfg<MODE, fm, fn, wgm, wgn, st, ks, DT, ASC>(a, s);
     KDL_PIPE_CONFIGS(KDL_PCASE)
 #undef KDL_PCASE
     default: return hipErrorInvalidValue;
@@ -303,6 +333,10 @@ hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& args, hipStream_t s)
   static const int env_krot = [] { const char* e = getenv("KDL_PIPE_KROT"); return e ? atoi(e) : -1; }();
   ConvGemmArgs a = args;
   if (env_krot >= 0) a.krot = env_krot;
+  if (a.ascale) {                             // A-operand channel scales: bf16 pointwise, whole K per tile
+    if (mode != 0 || a.dt != 0 || a.wimg || a.ksplit > 1) return hipErrorInvalidValue;
+    return launch_pipe_mode<0, 0, true>(cfg, a, s);
+  }
   if (mode == 0) return a.dt ? launch_pipe_mode<0, 1>(cfg, a, s) : launch_pipe_mode<0, 0>(cfg, a, s);
   if (mode == 1) return a.dt ? launch_pipe_mode<1, 1>(cfg, a, s) : launch_pipe_mode<1, 0>(cfg, a, s);
   return hipErrorInvalidValue;

@@ -59,6 +59,9 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
   constexpr int GS_NW = gs_waves<KT, NF>();
   __shared__ __attribute__((aligned(16))) uint8_t sB[NF * KT * 1024];
   __shared__ __attribute__((aligned(16))) float sBias[NF * 16];
+  // per-image A-operand channel scales of the loaded image (ConvGemmArgs.ascale: EfficientNet's SE
+  // scale on the project conv's input), applied to each A fragment in registers before its MFMAs
+  __shared__ __attribute__((aligned(16))) float sScale[KT * 32];
   // STG: staged stores (no residual, >= 2 fragment pairs; see the epilogue): a 16 x 144-byte tile per wave
   constexpr bool STG = !RES && NF >= 4;
   constexpr int GS_STG = 16 * 144;
@@ -78,7 +81,7 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
   // contiguous slice per workgroup made ~800 separate write streams and capped wide outputs at
   // 2.7 TB/s). Per-image weights: a contiguous slice per workgroup, walked image by image, so the
   // weights are reloaded only where the slice crosses an image.
-  const bool il = a.wimg == 0;
+  const bool il = a.wimg == 0 && !a.ascale;
   const int f0 = (int)((long)T * blockIdx.x / gridDim.x), f1 = (int)((long)T * (blockIdx.x + 1) / gridDim.x);
 
   for (int i = tid; i < NF * 16; i += 64 * GS_NW) sBias[i] = a.bias[i];
@@ -86,19 +89,23 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
   for (int fb = il ? 0 : f0; il ? fb == 0 : fb < f1;) {
     const int img = il ? 0 : fb / FPI;
     const int fend = il ? T : min(f1, (img + 1) * FPI);
-    if (loaded < 0 || (a.wimg && img != loaded)) {
+    if (loaded < 0 || (!il && img != loaded)) {
       __syncthreads();                               // the previous segment's waves are done with sB
       const uint16_t* wsrc = a.wp + (a.wimg ? (long)img * a.wimg : 0L);
       // fragment j, k-step t: KT consecutive KiB per fragment as in the packed [NF_pack][K/32][64][8]
       // layout, but with the output channels permuted inside each fragment pair (j even, j + 1): column
       // c of fragment j + h is channel 16 j + 8 (c / 4) + 4 h + c % 4, so accumulator lane quad g of the
       // pair holds the 8 consecutive channels 16 j + 8 g .. + 7 (one 16-byte store per lane)
+      // (shared weights with per-image scales: loaded once, only the scales change per image)
+      if (loaded < 0 || a.wimg)
       for (int i = tid; i < NF * KT * 64; i += 64 * GS_NW) {
         const int l = i & 63, jt = i >> 6, j = jt / KT, t = jt - j * KT, c = l & 15;
         const int ch = (j & ~1) * 16 + (c >> 2) * 8 + (j & 1) * 4 + (c & 3);
         const int src = ((ch >> 4) * KT + t) * 64 + ((ch & 15) | (l & 48));
         *(u32x4*)(sB + i * 16) = *(const u32x4*)(wsrc + (long)src * 8);
       }
+      if (a.ascale)
+        for (int i = tid; i < KT * 32; i += 64 * GS_NW) sScale[i] = a.ascale[(long)img * a.ascale_ld + i];
       __syncthreads();
       loaded = img;
     }
@@ -139,6 +146,20 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
         long mlim;
         const long m = row_of(q, mlim);
         const bool mok = m < mlim;
+        if (a.ascale) {                                // uniform: scale this fragment's A in place
+#pragma unroll
+          for (int t = 0; t < KT; ++t) {
+            const float* sc = sScale + t * 32 + kq * 8;
+            const f32x4 s0 = *(const f32x4*)sc, s1 = *(const f32x4*)(sc + 4);
+            const u32x4 u = __builtin_bit_cast(u32x4, ar[p][t]);
+            u32x4 o;
+            o[0] = pack_bf16(bf_lo(u[0]) * s0[0], bf_hi(u[0]) * s0[1]);
+            o[1] = pack_bf16(bf_lo(u[1]) * s0[2], bf_hi(u[1]) * s0[3]);
+            o[2] = pack_bf16(bf_lo(u[2]) * s1[0], bf_hi(u[2]) * s1[1]);
+            o[3] = pack_bf16(bf_lo(u[3]) * s1[2], bf_hi(u[3]) * s1[3]);
+            ar[p][t] = __builtin_bit_cast(s16x8, o);
+          }
+        }
         // the weight fragments are loop-invariant: an opaque lane offset keeps their LDS reads inside
         // the loop (hoisted, NF x KT fragments would take 4 x NF x KT VGPRs and spill)
         uint32_t boff = lane * 16;
@@ -281,6 +302,7 @@ hipError_t gemm_stream(const ConvGemmArgs& a, bool nt, hipStream_t s) {
   if (a.dt != 0 || a.opad || a.stride != 1 || a.ksplit > 1 || a.OH != a.H || a.OW != a.W || a.M <= 0 ||
       a.M != a.B * a.OH * a.OW || a.K % 32 != 0 || a.ldx % 8 != 0 || a.ldy % 8 != 0 || a.nstore % 8 != 0 ||
       (a.res && a.ldr % 8 != 0) || a.wimg < 0 || !gemm_stream_shape(a.K, a.nstore) ||
+      (a.ascale && (a.wimg || a.ascale_ld < a.K || a.ascale_ld % 4 != 0)) ||
       a.relu_out == 3 || a.relu_in || a.NF * 16 < a.nstore)
     return hipErrorInvalidValue;
   switch ((a.K / 32) * 100 + (a.nstore + 15) / 16) {

@@ -49,6 +49,12 @@ struct ConvGemmArgs {
   int ksplit;
   float* ws;
   int* cnt;
+  // per-image channel scales on the A operand (EfficientNet project conv: the SE scale, gemm_pipe
+  // MODE_PW bf16 only): A[m][k] is multiplied by ascale[image(m) * ascale_ld + k] on its way from
+  // LDS to the MFMA, so the shared weights serve every image; M tiles then never straddle two
+  // images (as with wimg). nullptr = no scale.
+  const float* ascale;
+  int ascale_ld;
 };
 
 // cfg < PIPE_CFG_BASE: register-B kernel (all modes, incl. fused depthwise);

@@ -273,10 +273,13 @@ def test_pool_add_batch_beyond_grid_y_limit():
 
 
 @pytest.mark.parametrize("HW,K,N", [(37 * 37, 480, 80), (19 * 19, 2304, 384), (150 * 150 // 9, 288, 48)])
-def test_per_image_weights_fold_channel_scale(HW, K, N):
-    """EfficientNet SE fold: weight_scale makes per-image copies of the packed project weights
-    scaled along k; the LDS-DMA GEMM with ConvGemmArgs.wimg (per-image M tiles) must equal
-    (D * s_b) W^T, every pipelined tile config."""
+@pytest.mark.parametrize("form", ["wimg", "ascale"])
+def test_per_image_weights_fold_channel_scale(HW, K, N, form):
+    """EfficientNet SE fold, every pipelined tile config, must equal (D * s_b) W^T:
+    wimg   weight_scale makes per-image copies of the packed project weights scaled along k; the
+           LDS-DMA GEMM with ConvGemmArgs.wimg (per-image M tiles) reads them;
+    ascale the LDS-DMA GEMM scales its A operand by ConvGemmArgs.ascale (per image and channel)
+           between LDS and the MFMAs, shared weights."""
     from kdl.ops.conv import PIPE_BASE, SEP_BASE
     gen = torch.Generator().manual_seed(9)
     B = 3
@@ -287,14 +290,19 @@ def test_per_image_weights_fold_channel_scale(HW, K, N):
     xs = (x.float().view(B, HW, lay.cin_pad) * sc[:, None, :]).to(torch.bfloat16).contiguous()
     ref = conv_gemm_ref(lay, xs.view(-1), g)
     per = lay.wp.numel()
-    wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
-    _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B, NF=lay.nf_max,
-                                 KT=lay.K // 32, C=K), _lib.stream_ptr())
+    kw = {}
+    if form == "wimg":
+        wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
+        _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B, NF=lay.nf_max,
+                                     KT=lay.K // 32, C=K), _lib.stream_ptr())
+        kw["wimg"] = (_lib.ptr(wimg), per)
+    else:
+        kw["ascale"] = (_lib.ptr(sc), K)
     cfgs = [c for _, c in lay.variants(1) if PIPE_BASE <= c < SEP_BASE]
     assert cfgs
     for cfg in cfgs:
         y = torch.full((g.M * lay.ldy,), float("nan"), dtype=torch.bfloat16, device=DEV)
-        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=cfg, wimg=(_lib.ptr(wimg), per))
+        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=cfg, **kw)
         torch.cuda.synchronize()
         try:
             _check(y, ref, N, tol=3e-2)
@@ -302,12 +310,30 @@ def test_per_image_weights_fold_channel_scale(HW, K, N):
             raise AssertionError(f"cfg={cfg}: {e}") from None
 
 
+def test_ascale_refused_off_the_pipelined_gemms():
+    """A-operand scales on a kernel that would ignore them (the register-B GEMM) fail loudly."""
+    gen = torch.Generator().manual_seed(3)
+    lay = _layer(MODE_PW, 64, 64, gen)
+    g = Geometry(2, 64, 1, 64, 1)
+    x = _rand_act((2, 64, 1), lay.cin_pad, 64, gen)
+    y = torch.zeros(g.M * lay.ldy, dtype=torch.bfloat16, device=DEV)
+    sc = torch.ones(2, 64, device=DEV)
+    lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=0)          # the same launch without scales runs
+    torch.cuda.synchronize()
+    with pytest.raises(AssertionError):
+        lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, cfg=0, ascale=(_lib.ptr(sc), 64))
+    ga = lay.args(_lib.ptr(x), _lib.ptr(y), g, None, cfg=0)
+    ga.update(ascale=_lib.ptr(sc), ascale_ld=64)
+    with pytest.raises(RuntimeError):
+        _lib.lib().conv_gemm(MODE_PW, 0, ga, _lib.stream_ptr())
+
+
 # (K, n) of every streaming-GEMM instance (EfficientNet-B7's large-map expand / project convs)
 STREAM_KN = [(32, 32), (64, 32), (32, 192), (192, 48), (64, 288), (288, 48), (288, 80), (96, 480), (480, 80)]
 
 
 @pytest.mark.parametrize("K,N", STREAM_KN)
-@pytest.mark.parametrize("kind", ["silu", "wimg_res"])
+@pytest.mark.parametrize("kind", ["silu", "wimg_res", "ascale_res"])
 @pytest.mark.parametrize("nt", [False, True])
 def test_gemm_stream(K, N, kind, nt):
     """Streaming pointwise GEMM (gemm_stream.hip, id STREAM_BASE) against the fp32 reference: the
@@ -334,12 +360,16 @@ def test_gemm_stream(K, N, kind, nt):
         sc = (torch.rand(B, K, generator=gen) + 0.25).to(DEV)
         xs = (x.float().view(B, H * H, lay.cin_pad) * sc[:, None, :]).to(torch.bfloat16).contiguous()
         ref = conv_gemm_ref(lay, xs.view(-1), g, res=res)
-        per = lay.wp.numel()
-        wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
-        _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B, NF=lay.nf_max,
-                                     KT=lay.K // 32, C=K), _lib.stream_ptr())
+        if kind == "ascale_res":                # shared weights, the scales on the A operand
+            kw = dict(ascale=(_lib.ptr(sc), K))
+        else:
+            per = lay.wp.numel()
+            wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
+            _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B,
+                                         NF=lay.nf_max, KT=lay.K // 32, C=K), _lib.stream_ptr())
+            kw = dict(wimg=(_lib.ptr(wimg), per))
         lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, res=_lib.ptr(res) if res is not None else None, cfg=cfg,
-                 wimg=(_lib.ptr(wimg), per))
+                 **kw)
     torch.cuda.synchronize()
     _check(y, ref, N, tol=3e-2)
 
