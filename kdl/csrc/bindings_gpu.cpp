@@ -44,7 +44,6 @@ ConvGemmArgs conv_args(const py::dict& d) {
   a.nstore = I(d, "nstore"); a.stride = I(d, "stride", 1);
   a.relu_in = I(d, "relu_in"); a.relu_out = I(d, "relu_out"); a.opad = I(d, "opad");
   a.dt = I(d, "dt");
-  a.wimg = I(d, "wimg");
   a.krot = I(d, "krot");
   a.ksplit = I(d, "ksplit");
   a.ws = P<float>(d, "ws");
@@ -138,12 +137,6 @@ ChScaleArgs chs_args(const py::dict& d) {
   ChScaleArgs a{};
   a.y = P<uint16_t>(d, "y"); a.scale = P<const float>(d, "scale");
   a.B = I(d, "B"); a.HW = I(d, "HW"); a.C = I(d, "C");
-  return a;
-}
-WScaleArgs ws_args(const py::dict& d) {
-  WScaleArgs a{};
-  a.w = P<const uint16_t>(d, "w"); a.scale = P<const float>(d, "scale"); a.y = P<uint16_t>(d, "y");
-  a.B = I(d, "B"); a.NF = I(d, "NF"); a.KT = I(d, "KT"); a.C = I(d, "C");
   return a;
 }
 GemmF8Args f8_args(const py::dict& d) {
@@ -310,11 +303,6 @@ PYBIND11_MODULE(_C, m) {
     const auto a = chs_args(d);
     py::gil_scoped_release nogil;
     chk(channel_scale(a, S(s)), "channel_scale");
-  });
-  m.def("weight_scale", [](py::dict d, uintptr_t s) {
-    const auto a = ws_args(d);
-    py::gil_scoped_release nogil;
-    chk(weight_scale(a, S(s)), "weight_scale");
   });
   m.def("entry_block", [](int cfg, py::dict d, uintptr_t s) {
     const auto a = eb_args(d);
@@ -551,9 +539,6 @@ PYBIND11_MODULE(_C, m) {
       })
       .def("add_se", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_SE; op.name = name; op.se = se_args(d); p.add(op);
-      })
-      .def("add_wscale", [](Program& p, const std::string& name, py::dict d) {
-        Op op; op.kind = OP_WSCALE; op.name = name; op.ws = ws_args(d); p.add(op);
       })
       .def("add_chscale", [](Program& p, const std::string& name, py::dict d) {
         Op op; op.kind = OP_CHSCALE; op.name = name; op.cs = chs_args(d); p.add(op);

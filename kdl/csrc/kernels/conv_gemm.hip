@@ -297,9 +297,8 @@ hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s) {
   if (cfg >= STREAM_CFG_BASE)
     return mode == MODE_PW && cfg <= STREAM_CFG_BASE + 1 ? gemm_stream(a, cfg == STREAM_CFG_BASE + 1, s)
                                                          : hipErrorInvalidValue;
-  // split-K and per-image weights: the LDS-DMA pipelined GEMM only
+  // split-K: the LDS-DMA pipelined GEMM only
   if (a.ksplit > 1 && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE)) return hipErrorInvalidValue;
-  if (a.wimg && (cfg < PIPE_CFG_BASE || cfg >= SEP_CFG_BASE || a.wimg < 0)) return hipErrorInvalidValue;
   if (a.dt == 1) {   // fp16: the pointwise / implicit-3x3 GEMMs only
     if (cfg >= SEP_CFG_BASE) return hipErrorInvalidValue;
     if (cfg >= PIPE_CFG_BASE) return gemm_pipe(mode, cfg - PIPE_CFG_BASE, a, s);

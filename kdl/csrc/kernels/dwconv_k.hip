@@ -625,36 +625,5 @@ hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- SE scale -> weights
-// Folding the squeeze-excite scale into the project conv: (D * s_b) W^T = D (W * s_b)^T, so
-// instead of rewriting the whole depthwise output D in place (chscale: read + write of the
-// largest tensors of the network) each image gets its own copy of the packed project
-// weights scaled along k -- N x K per image, ~1000x fewer bytes in the early stages.
-// One thread = one 16-byte lane slot (8 consecutive k of one output channel).
-__global__ __launch_bounds__(256) void wscale_kernel(WScaleArgs a) {
-  const long per = (long)a.NF * a.KT * 64;     // 16-byte slots per image
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= per) return;
-  const int b = blockIdx.y;
-  const int lane = (int)(i & 63);
-  const int t = (int)((i >> 6) % a.KT);
-  const int k0 = t * 32 + (lane >> 4) * 8;
-  const float4* sc = (const float4*)(a.scale + (long)b * a.C + k0);
-  const float4 s0 = sc[0], s1 = sc[1];
-  u32x4 v = *(const u32x4*)(a.w + i * 8);
-  v[0] = pack_bf16(bf_lo(v[0]) * s0.x, bf_hi(v[0]) * s0.y);
-  v[1] = pack_bf16(bf_lo(v[1]) * s0.z, bf_hi(v[1]) * s0.w);
-  v[2] = pack_bf16(bf_lo(v[2]) * s1.x, bf_hi(v[2]) * s1.y);
-  v[3] = pack_bf16(bf_lo(v[3]) * s1.z, bf_hi(v[3]) * s1.w);
-  *(u32x4*)(a.y + ((long)b * per + i) * 8) = v;
-}
-
-hipError_t weight_scale(const WScaleArgs& a, hipStream_t s) {
-  if (a.B <= 0 || a.B > 65535 || a.NF <= 0 || a.KT <= 0 || a.C < 32 * a.KT || a.C % 4 != 0)
-    return hipErrorInvalidValue;
-  const long per = (long)a.NF * a.KT * 64;
-  hipLaunchKernelGGL(wscale_kernel, dim3((unsigned)((per + 255) / 256), (unsigned)a.B), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
 
 }  // namespace kdl

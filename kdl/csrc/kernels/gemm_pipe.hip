@@ -68,9 +68,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   const int wm = wave / WGN, wn = wave % WGN;
   const int nN = (a.NF * 16) / BN;
   const int OHW = a.OH * a.OW;
-  // per-image weights (a.wimg) or A scales (ASC): M tiles are cut per image so a tile has one
-  // weight set / one scale vector
-  const bool per_img = a.wimg || ASC;
+  // A scales (ASC): M tiles are cut per image so a tile has one scale vector
+  constexpr bool per_img = ASC;
   const int mpi = per_img ? (OHW + BM - 1) / BM : 0;
   const int nM = per_img ? a.B * mpi : (a.M + BM - 1) / BM;
   // split-K: consecutive logical ids are the splits of one tile (same XCD: their partials meet in L2)
@@ -80,13 +79,11 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
   const int ksid = wid % S, tile = wid / S;
   const int mi = tile / nN, ni = tile % nN;
   int m0 = mi * BM, mend = a.M;
-  long wofs = 0;
   int bi = 0;
   if (per_img) {
     bi = mi / mpi;
     m0 = bi * OHW + (mi - bi * mpi) * BM;
     mend = (bi + 1) * OHW;
-    wofs = (long)bi * a.wimg;
   }
   const int n0 = ni * BN;
   const int KT32 = (a.K >> 5) / S;           // 32-deep k steps of this split (host: divisible)
@@ -107,7 +104,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       src[i] = pix * a.ldx + 8 * (lane >> 4);
     } else if (f < FRD) {
       const int nf = n0 / 16 + (f - AF);
-      src[i] = wofs + ((long)nf * (a.K >> 5)) * 512 + lane * 8;
+      src[i] = ((long)nf * (a.K >> 5)) * 512 + lane * 8;
     } else {                                  // ASC: 8 lanes x 16 B = the k-step's 32 scales, repeated
       src[i] = (long)bi * a.ascale_ld + (lane & 7) * 4;
     }
@@ -306,7 +303,7 @@ template <int MODE, int FM, int FN, int WGM, int WGN, int ST, int KS, int DT = 0
 static hipError_t launch_pipe_cfg(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   if ((a.NF * 16) % BN != 0) return hipErrorInvalidValue;
-  const bool per_img = a.wimg || ASC;
+  constexpr bool per_img = ASC;
   if (per_img && (a.M != a.B * a.OH * a.OW || a.B <= 0)) return hipErrorInvalidValue;
   if (ASC && (!a.ascale || a.ascale_ld < a.K || a.ascale_ld % 4 != 0)) return hipErrorInvalidValue;
   const int nM = per_img ? a.B * ((a.OH * a.OW + BM - 1) / BM) : (a.M + BM - 1) / BM, nN = (a.NF * 16) / BN;
@@ -334,7 +331,7 @@ hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& args, hipStream_t s)
   ConvGemmArgs a = args;
   if (env_krot >= 0) a.krot = env_krot;
   if (a.ascale) {                             // A-operand channel scales: bf16 pointwise, whole K per tile
-    if (mode != 0 || a.dt != 0 || a.wimg || a.ksplit > 1) return hipErrorInvalidValue;
+    if (mode != 0 || a.dt != 0 || a.ksplit > 1) return hipErrorInvalidValue;
     return launch_pipe_mode<0, 0, true>(cfg, a, s);
   }
   if (mode == 0) return a.dt ? launch_pipe_mode<0, 1>(cfg, a, s) : launch_pipe_mode<0, 0>(cfg, a, s);

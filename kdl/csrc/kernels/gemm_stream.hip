@@ -7,7 +7,7 @@
 // (tools/layer_profile.py --model efficientnet_b7, round 5). Here:
 //   * persistent workgroups of 8 or 16 waves, one round of them (occupancy-sized grid); the whole weight matrix (NF fragments x KT k-steps, fragment-
 //     linear, <= 90 KiB) and the bias sit in LDS for the kernel's life (reloaded only when a
-//     workgroup's row range crosses into the next image's per-image weights, ConvGemmArgs.wimg);
+//     workgroup's row range crosses into the next image's A-operand scales, ConvGemmArgs.ascale);
 //   * every wave streams 16-row A fragments straight from HBM into registers, PD fragments ahead
 //     (register ring), so each CU keeps ~16 x PD x KT KiB of reads in flight;
 //   * per row fragment, the NF output fragments are computed two at a time (MFMA 16x16x32 with the
@@ -81,7 +81,7 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
   // contiguous slice per workgroup made ~800 separate write streams and capped wide outputs at
   // 2.7 TB/s). Per-image weights: a contiguous slice per workgroup, walked image by image, so the
   // weights are reloaded only where the slice crosses an image.
-  const bool il = a.wimg == 0 && !a.ascale;
+  const bool il = !a.ascale;
   const int f0 = (int)((long)T * blockIdx.x / gridDim.x), f1 = (int)((long)T * (blockIdx.x + 1) / gridDim.x);
 
   for (int i = tid; i < NF * 16; i += 64 * GS_NW) sBias[i] = a.bias[i];
@@ -91,13 +91,13 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
     const int fend = il ? T : min(f1, (img + 1) * FPI);
     if (loaded < 0 || (!il && img != loaded)) {
       __syncthreads();                               // the previous segment's waves are done with sB
-      const uint16_t* wsrc = a.wp + (a.wimg ? (long)img * a.wimg : 0L);
+      const uint16_t* wsrc = a.wp;
       // fragment j, k-step t: KT consecutive KiB per fragment as in the packed [NF_pack][K/32][64][8]
       // layout, but with the output channels permuted inside each fragment pair (j even, j + 1): column
       // c of fragment j + h is channel 16 j + 8 (c / 4) + 4 h + c % 4, so accumulator lane quad g of the
       // pair holds the 8 consecutive channels 16 j + 8 g .. + 7 (one 16-byte store per lane)
-      // (shared weights with per-image scales: loaded once, only the scales change per image)
-      if (loaded < 0 || a.wimg)
+      // (per-image scales: the weights are loaded once, only the scales change per image)
+      if (loaded < 0)
       for (int i = tid; i < NF * KT * 64; i += 64 * GS_NW) {
         const int l = i & 63, jt = i >> 6, j = jt / KT, t = jt - j * KT, c = l & 15;
         const int ch = (j & ~1) * 16 + (c >> 2) * 8 + (j & 1) * 4 + (c & 3);
@@ -301,8 +301,8 @@ bool gemm_stream_shape(int K, int nstore) {
 hipError_t gemm_stream(const ConvGemmArgs& a, bool nt, hipStream_t s) {
   if (a.dt != 0 || a.opad || a.stride != 1 || a.ksplit > 1 || a.OH != a.H || a.OW != a.W || a.M <= 0 ||
       a.M != a.B * a.OH * a.OW || a.K % 32 != 0 || a.ldx % 8 != 0 || a.ldy % 8 != 0 || a.nstore % 8 != 0 ||
-      (a.res && a.ldr % 8 != 0) || a.wimg < 0 || !gemm_stream_shape(a.K, a.nstore) ||
-      (a.ascale && (a.wimg || a.ascale_ld < a.K || a.ascale_ld % 4 != 0)) ||
+      (a.res && a.ldr % 8 != 0) || !gemm_stream_shape(a.K, a.nstore) ||
+      (a.ascale && (a.ascale_ld < a.K || a.ascale_ld % 4 != 0)) ||
       a.relu_out == 3 || a.relu_in || a.NF * 16 < a.nstore)
     return hipErrorInvalidValue;
   switch ((a.K / 32) * 100 + (a.nstore + 15) / 16) {

@@ -33,10 +33,6 @@ struct ConvGemmArgs {
                          //    next 3x3 'same' conv runs as a 'valid' implicit GEMM with no bounds checks;
                          // 2: token rows behind a class token: row m -> b*(OH*OW+1) + 1 + m%(OH*OW)
   int dt;                // element type of x / wp / res / y: 0 bf16, 1 fp16 (MODE_PW / MODE_CONV GEMMs)
-  // per-image weights (EfficientNet project conv with the SE channel scale folded in, gemm_pipe
-  // only): wp points at [B][NF][K/32][64][8] and wimg is the element stride between images;
-  // M tiles then never straddle two images. 0 = one weight set for every row.
-  int wimg;
   // LDS-DMA pipelined GEMM (gemm_pipe): 1 = every M tile walks K from its own starting
   // step ((7*mi) mod K/32), so the workgroups sharing the weights do not all fetch the same
   // fragments at launch (env KDL_PIPE_KROT overrides; 0 = in order)
@@ -51,8 +47,8 @@ struct ConvGemmArgs {
   int* cnt;
   // per-image channel scales on the A operand (EfficientNet project conv: the SE scale, gemm_pipe
   // MODE_PW bf16 only): A[m][k] is multiplied by ascale[image(m) * ascale_ld + k] on its way from
-  // LDS to the MFMA, so the shared weights serve every image; M tiles then never straddle two
-  // images (as with wimg). nullptr = no scale.
+  // LDS to the MFMA (round 6; it replaced per-image SE-scaled weight copies); M tiles then never
+  // straddle two images. nullptr = no scale.
   const float* ascale;
   int ascale_ld;
 };
@@ -279,16 +275,6 @@ struct ChScaleArgs {
   int B, HW, C;
 };
 hipError_t channel_scale(const ChScaleArgs& a, hipStream_t s);
-
-// SE scale folded into the project conv's weights: y[b] = w * scale[b][k] for every element of
-// the packed fragments w [NF][KT][64][8] (k = 32 t + 8 (lane >> 4) + e), bf16.
-struct WScaleArgs {
-  const uint16_t* w;      // [NF][KT][64][8]
-  const float* scale;     // [B][C]
-  uint16_t* y;            // [B][NF][KT][64][8]
-  int B, NF, KT, C;       // C: scale row stride (>= 32 KT)
-};
-hipError_t weight_scale(const WScaleArgs& a, hipStream_t s);
 
 // FP8 (OCP e4m3) GEMM, gemm_f8.hip: y = act(colscale[n] * A8 W8^T + bias[n]) (+res), bf16 or fp8 out.
 struct GemmF8Args {

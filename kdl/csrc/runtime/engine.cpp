@@ -27,7 +27,6 @@ hipError_t run_op(const Op& op, hipStream_t s) {
     case OP_DWK: return dwk(op.dk, s);
     case OP_SE: return squeeze_excite(op.se, s);
     case OP_CHSCALE: return channel_scale(op.cs, s);
-    case OP_WSCALE: return weight_scale(op.ws, s);
     case OP_GEMM_F8: return gemm_f8(op.cfg, op.f8, s);
     case OP_ENTRY_BLOCK: return entry_block(op.cfg, op.eb, s);
   }

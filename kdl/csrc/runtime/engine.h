@@ -17,9 +17,11 @@ namespace kdl {
 
 enum OpKind { OP_CONV_GEMM = 0, OP_STEM = 1, OP_POOL_ADD = 2, OP_HEAD = 3, OP_RESIZE = 4, OP_MEMSET = 5, OP_DW = 6, OP_GAP = 7, OP_FC = 8, OP_FC_MFMA = 9,
               OP_PATCHIFY = 10, OP_EMBED = 11, OP_LN = 12, OP_ATTN = 13,
-              OP_DWK = 14, OP_SE = 15, OP_CHSCALE = 16, OP_GEMM_F8 = 17, OP_WSCALE = 18,
-              OP_ENTRY_BLOCK = 21 };   // 19: retired (the round-3 chained middle-flow launch); 20: retired
-                                       // (round 5: the vendor GEMM node left the product, tools/probes/blaslt)
+              OP_DWK = 14, OP_SE = 15, OP_CHSCALE = 16, OP_GEMM_F8 = 17,
+              OP_ENTRY_BLOCK = 21 };   // 18: retired (round 6: the SE weight scale, replaced by the project
+                                       // GEMM's A-operand scales); 19: retired (the round-3 chained
+                                       // middle-flow launch); 20: retired (round 5: the vendor GEMM node
+                                       // left the product, tools/probes/blaslt)
 
 struct Op {
   OpKind kind;
@@ -41,7 +43,6 @@ struct Op {
   DwkArgs dk{};
   SeArgs se{};
   ChScaleArgs cs{};
-  WScaleArgs ws{};
   GemmF8Args f8{};
   EntryBlockArgs eb{};
   void* mem_ptr = nullptr;

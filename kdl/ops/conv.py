@@ -273,10 +273,8 @@ class ConvGemmLayer:
     def emit(self, prog, x: int, y: int, g: Geometry, res: int | None = None, ldx: int | None = None,
              ldr: int | None = None, tmp: int | None = None, split: bool | None = None,
              cfg: int | None = None, opad: int = 0,
-             wimg: tuple[int, int] | None = None, ascale: tuple[int, int] | None = None) -> None:
+             ascale: tuple[int, int] | None = None) -> None:
         """Append this layer's launches to a native Program (or launch now if prog is None).
-        ``wimg``: (pointer, per-image element stride) of
-        per-image copies of the packed weights (ConvGemmArgs.wimg; LDS-DMA GEMM configs only).
         ``ascale``: (pointer, per-image stride) of fp32 per-image channel scales applied to the A
         operand (ConvGemmArgs.ascale; LDS-DMA / streaming GEMM configs, bf16 pointwise only)."""
         split = self.split if split is None else split
@@ -302,7 +300,7 @@ class ConvGemmLayer:
             return
         if is_splitk(cfg):
             sk, cfg = splitk_parts(cfg)
-            assert wimg is None and (self.K // 32) % sk == 0, (self.name, sk)
+            assert ascale is None and (self.K // 32) % sk == 0, (self.name, sk)
             ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
             ws, cnt = self._splitk_workspace(sk, cfg, g.M)
             ga.update(ksplit=sk, ws=_lib.ptr(ws), cnt=_lib.ptr(cnt))
@@ -312,13 +310,9 @@ class ConvGemmLayer:
                 prog.add_conv_gemm(self.name, self.mode, cfg, ga)
             return
         ga = self.args(x, y, g, res, ldx=ldx, ldr=ldr, cfg=cfg, opad=opad)
-        if wimg:
-            assert PIPE_BASE <= cfg < SEP_BASE or cfg in STREAM_IDS, \
-                "per-image weights ride the LDS-DMA pipelined GEMM or the streaming GEMM"
-            ga.update(wp=wimg[0], wimg=wimg[1])
         if ascale:
             assert (PIPE_BASE <= cfg < SEP_BASE or cfg in STREAM_IDS) and self.mode == MODE_PW and \
-                self.dt == 0 and not wimg, \
+                self.dt == 0, \
                 "A-operand channel scales ride the bf16 pointwise LDS-DMA pipelined or streaming GEMM"
             ga.update(ascale=ascale[0], ascale_ld=ascale[1])
         if prog is None:

@@ -273,13 +273,10 @@ def test_pool_add_batch_beyond_grid_y_limit():
 
 
 @pytest.mark.parametrize("HW,K,N", [(37 * 37, 480, 80), (19 * 19, 2304, 384), (150 * 150 // 9, 288, 48)])
-@pytest.mark.parametrize("form", ["wimg", "ascale"])
-def test_per_image_weights_fold_channel_scale(HW, K, N, form):
-    """EfficientNet SE fold, every pipelined tile config, must equal (D * s_b) W^T:
-    wimg   weight_scale makes per-image copies of the packed project weights scaled along k; the
-           LDS-DMA GEMM with ConvGemmArgs.wimg (per-image M tiles) reads them;
-    ascale the LDS-DMA GEMM scales its A operand by ConvGemmArgs.ascale (per image and channel)
-           between LDS and the MFMAs, shared weights."""
+def test_ascale_fold_channel_scale(HW, K, N):
+    """EfficientNet SE scale on the project GEMM: the LDS-DMA GEMM scales its A operand by
+    ConvGemmArgs.ascale (per image and channel, per-image M tiles) between LDS and the MFMAs;
+    every pipelined tile config must equal (D * s_b) W^T."""
     from kdl.ops.conv import PIPE_BASE, SEP_BASE
     gen = torch.Generator().manual_seed(9)
     B = 3
@@ -289,15 +286,7 @@ def test_per_image_weights_fold_channel_scale(HW, K, N, form):
     sc = (torch.rand(B, K, generator=gen) + 0.25).to(DEV)
     xs = (x.float().view(B, HW, lay.cin_pad) * sc[:, None, :]).to(torch.bfloat16).contiguous()
     ref = conv_gemm_ref(lay, xs.view(-1), g)
-    per = lay.wp.numel()
-    kw = {}
-    if form == "wimg":
-        wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
-        _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B, NF=lay.nf_max,
-                                     KT=lay.K // 32, C=K), _lib.stream_ptr())
-        kw["wimg"] = (_lib.ptr(wimg), per)
-    else:
-        kw["ascale"] = (_lib.ptr(sc), K)
+    kw = dict(ascale=(_lib.ptr(sc), K))
     cfgs = [c for _, c in lay.variants(1) if PIPE_BASE <= c < SEP_BASE]
     assert cfgs
     for cfg in cfgs:
@@ -333,11 +322,11 @@ STREAM_KN = [(32, 32), (64, 32), (32, 192), (192, 48), (64, 288), (288, 48), (28
 
 
 @pytest.mark.parametrize("K,N", STREAM_KN)
-@pytest.mark.parametrize("kind", ["silu", "wimg_res", "ascale_res"])
+@pytest.mark.parametrize("kind", ["silu", "ascale_res"])
 @pytest.mark.parametrize("nt", [False, True])
 def test_gemm_stream(K, N, kind, nt):
     """Streaming pointwise GEMM (gemm_stream.hip, id STREAM_BASE) against the fp32 reference: the
-    expand form (SiLU epilogue, shared weights) and the project form (per-image SE-scaled weights,
+    expand form (SiLU epilogue) and the project form (per-image SE scales on the A operand,
     residual add), on a ragged 37x37 map (partial 16-row fragments, images crossing workgroups);
     both the plain and the nontemporal-store ids."""
     from kdl.ops.conv import STREAM_BASE, STREAM_NT
@@ -360,14 +349,7 @@ def test_gemm_stream(K, N, kind, nt):
         sc = (torch.rand(B, K, generator=gen) + 0.25).to(DEV)
         xs = (x.float().view(B, H * H, lay.cin_pad) * sc[:, None, :]).to(torch.bfloat16).contiguous()
         ref = conv_gemm_ref(lay, xs.view(-1), g, res=res)
-        if kind == "ascale_res":                # shared weights, the scales on the A operand
-            kw = dict(ascale=(_lib.ptr(sc), K))
-        else:
-            per = lay.wp.numel()
-            wimg = torch.zeros(B * per, dtype=torch.bfloat16, device=DEV)
-            _lib.lib().weight_scale(dict(w=_lib.ptr(lay.wp), scale=_lib.ptr(sc), y=_lib.ptr(wimg), B=B,
-                                         NF=lay.nf_max, KT=lay.K // 32, C=K), _lib.stream_ptr())
-            kw = dict(wimg=(_lib.ptr(wimg), per))
+        kw = dict(ascale=(_lib.ptr(sc), K))
         lay.emit(None, _lib.ptr(x), _lib.ptr(y), g, res=_lib.ptr(res) if res is not None else None, cfg=cfg,
                  **kw)
     torch.cuda.synchronize()

@@ -6,8 +6,8 @@ Oracles (torch, any device), all from the same folded parameters:
   fp32        models/efficientnet.py's forward (BN folded in float64, applied in fp32)
   bf16        rounds to bf16 exactly where the engine stores bf16: the stem / expand / depthwise /
               project outputs and the folded weights, the SE-scaled project input bf16(D * s)
-              (engine/efficientnet.py, KDL_SEFOLD=2; with KDL_SEFOLD=1 the per-image bf16
-              project weights of "wscale"), the pooled head features
+              (engine/efficientnet.py: the scale on the project GEMM's A operand), the pooled
+              head features
   bf16+f32res the bf16 oracle with the block outputs (the residual stream) kept in fp32
   fp32+noise  the fp32 oracle on an input perturbed by ~bf16 rounding noise at the stem output
               (how much this random-init network amplifies a 2^-9 relative perturbation)
@@ -67,11 +67,6 @@ def stem(F_, x_u8, mode):
     return bf(y) if mode != "fp32" else y
 
 
-# where the engine applies the SE scale (kdl/engine/efficientnet.py, env KDL_SEFOLD): 2 = on the
-# project GEMM's A operand (default), 1 = folded into per-image bf16 weights ("wscale")
-SEFOLD = int(os.environ.get("KDL_SEFOLD", "2"))
-
-
 def block(b, d, x, mode, res_f32=False):
     """One MBConv; mode fp32 | bf16 (engine rounding points)."""
     r = (lambda t: t) if mode == "fp32" else bf
@@ -90,9 +85,6 @@ def block(b, d, x, mode, res_f32=False):
     wp = wp.view(b.cout, b.cexp)
     if mode == "fp32":
         out = torch.einsum("bchw,oc->bohw", D * s[:, :, None, None], wp)
-    elif SEFOLD == 1:                                          # per-image bf16(W * s) (engine "wscale")
-        wimg = bf(bf(wp)[None] * s[:, None, :])                # [B, cout, cexp]
-        out = torch.einsum("bchw,boc->bohw", D, wimg)
     else:                                                      # bf16(D * s) on the GEMM's A operand
         out = torch.einsum("bchw,oc->bohw", bf(D * s[:, :, None, None]), bf(wp))
     out = out + tp.view(1, -1, 1, 1)
