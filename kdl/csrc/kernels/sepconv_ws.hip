@@ -241,6 +241,13 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
     // load them (round 6) put a branch into the loop body, and hipcc then stopped hoisting the
     // depthwise MFMAs above the barrier (one basic block each side): +2 us per no-ReLU layer
     auto issue = [&](int t, int slot) { glds16(wsrc + (long)kc(t) * 1024, smem + slot * STAGE + WOFF); };
+    // the weight DMAs of the first stages go out BEFORE the tap-offset setup below (its runtime
+    // divisions by W and H take ~1,400 cycles): the prologue barrier waits for them. Issued after the
+    // setup (until round 6), the prologue ran 8,760 instead of 6,892 cycles (stamped ZF build,
+    // mid_sep_nr) and the bench read 0.6 % lower in 3 of 3 pairs (profiles/middle_flow_r6.txt)
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; ++p) issue(p, p);
+    pstamp(1);
 
     const int g = pw & 1;                        // channel group of all this wave's units
     const int p16 = lane & 15, kb = lane >> 4;
@@ -353,9 +360,6 @@ __device__ __forceinline__ void ws_tile(const ConvGemmArgs& a, int mi, int ni, u
     };
 
     pstamp(0);                                   // setup (tap offsets) done
-#pragma unroll
-    for (int p = 0; p < STAGES - 1; ++p) issue(p, p);
-    pstamp(1);
     if constexpr (ZF) {                          // the stages' zero blocks: 16 x 16 B each
       const int z = pw * 64 + lane;
       if (z < STAGES * 16) *(u32x4*)(smem + (z >> 4) * STAGE + ZOFF + (z & 15) * 16) = (u32x4){0u, 0u, 0u, 0u};
