@@ -136,6 +136,12 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--depth", type=int, default=3,
                     help="ingress prefetch distance in batches (input slots = depth + 1 + slack)")
+    ap.add_argument("--settle-mode", choices=["pipe", "serial"], default="pipe",
+                    help="DIAGNOSTIC: what the settle phase runs -- the pipelined step (default) or joined graph "
+                         "replays (the pre-round-6 settle)")
+    ap.add_argument("--touch", choices=["auto", "on", "off"], default="auto",
+                    help="one joined replay before the inputs are primed, so the pipeline-stage streams submit before "
+                         "the copy stream (hardware-queue mapping order); auto = on for 3+ stages")
     ap.add_argument("--timeline", action="store_true",
                     help="DIAGNOSTIC: timing events around every pipeline stage of the timed steps; prints per-stage "
                          "busy / overlap / idle to stderr (the events sit inside the timed window)")
@@ -411,16 +417,29 @@ def main(argv=None) -> int:
     # round 6, but the pipelined regime kept speeding up for ~60 steps after them (20 steps after
     # 5 warmup steps read 1.28 ms/step, after 60 warmup steps 1.254: profiles/bench_settle_r6.txt).
     # Ranks agree on every chunk (a step may hold collectives), so all run the same count.
-    for i in range(a.depth):
-        ingress(i)
+    if a.settle_mode == "pipe":
+        # one joined replay first, so every pipeline-stage stream submits work before the ingress copy
+        # stream does: HIP binds streams to its GPU_MAX_HW_QUEUES (4 on the box) hardware queues in
+        # first-use order. With the copies first, ResNet-50's three stages + the copy stream read 17 %
+        # lower (32.5k vs 39.1k img/s); Xception's two stages read 0.4 % higher that way, so the touch
+        # is on for 3+ stages only (profiles/bench_settle_r6.txt)
+        touch = a.touch == "on" or (a.touch == "auto" and len(getattr(eng, "ranges", ())) >= 3)
+        if touch:
+            eng.launch(B, s, capture=use_graph)
+            torch.cuda.synchronize()
+        for i in range(a.depth):
+            ingress(i)
     nxt = 0
     t_start = time.perf_counter()
     chunk_ms: list[float] = []
     while True:
         c0 = time.perf_counter()
         for _ in range(10):
-            step(nxt)
-            nxt += 1
+            if a.settle_mode == "pipe":
+                step(nxt)
+                nxt += 1
+            else:
+                eng.launch(B, s, capture=use_graph)
         torch.cuda.synchronize()
         chunk_ms.append((time.perf_counter() - c0) * 1e3)
         spent = time.perf_counter() - t_start
@@ -435,6 +454,9 @@ def main(argv=None) -> int:
     settle_s = time.perf_counter() - t_start
     if rank == 0:   # settle trajectory of the untimed pipelined steps (fresh-lease diagnosis, stderr only)
         print("settle chunks (10 pipelined steps, ms): " + " ".join(f"{c:.2f}" for c in chunk_ms), file=sys.stderr)
+    if a.settle_mode != "pipe":
+        for i in range(a.depth):
+            ingress(i)
     if dist_on:
         dist.barrier()
     for i in range(nxt, nxt + a.warmup):
