@@ -13,9 +13,10 @@
 //   * per row fragment, the NF output fragments are computed two at a time (MFMA 16x16x32 with the
 //     weight fragment as the first operand: each lane holds 4 consecutive output channels of one
 //     row) and stored from the accumulators (8 bytes per lane: bias, SiLU / ReLU, residual fused) --
-//     no C tile through LDS, no barrier in the loop.
-// Instances per (KT, NF) -- the B7 shapes; any other shape is refused (hipErrorInvalidValue) and the
-// layer keeps its tiled configs.
+//     no C tile through LDS, no barrier in the loop;
+//   * opad 1 (ResNet's conv1 feeding a 'valid' 3x3): rows land in the interior of a zero-bordered buffer.
+// Instances per (KT, NF) -- the B7 shapes (bf16) and ResNet-50's layer1 / layer2 1x1 convs (fp16, DT 1);
+// any other shape is refused (hipErrorInvalidValue) and the layer keeps its tiled configs.
 #include "common.h"
 #include "launch.h"
 
@@ -53,8 +54,10 @@ constexpr int gs_waves() { return gs_lds<KT, NF>() > 53 * 1024 ? 16 : 8; }
 // NT: nontemporal output stores (streaming cache policy). Measured (tools/stream_ab.py, B7 b32): a win for
 // outputs well past the 256 MB MALL (the 150x150 expands: 177 -> 138 us), a loss for ones the next layer
 // can still find cached (the residual projects: 134 -> 143 us) -- a separate config id, picked by the tuner
-template <int KT, int NF, bool RES, bool NT, int ACT>
+// DT: element type of x / weights / residual / y (common.h Elt: 0 bf16, 1 fp16)
+template <int KT, int NF, bool RES, bool NT, int ACT, int DT = 0>
 __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(ConvGemmArgs a) {
+  using E = Elt<DT>;
   constexpr int PD = gs_prefetch<KT, NF, RES>();
   constexpr int GS_NW = gs_waves<KT, NF>();
   __shared__ __attribute__((aligned(16))) uint8_t sB[NF * KT * 1024];
@@ -146,7 +149,7 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
         long mlim;
         const long m = row_of(q, mlim);
         const bool mok = m < mlim;
-        if (a.ascale) {                                // uniform: scale this fragment's A in place
+        if (DT == 0 && a.ascale) {                     // uniform: scale this fragment's A in place (bf16)
 #pragma unroll
           for (int t = 0; t < KT; ++t) {
             const float* sc = sScale + t * 32 + kq * 8;
@@ -172,7 +175,7 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj)
               if (j0 + jj < NF)
-                acc[jj] = mfma16(*(const s16x8*)(sB + ((j0 + jj) * KT + t) * 1024 + boff), ar[p][t], acc[jj]);
+                acc[jj] = E::mfma(*(const s16x8*)(sB + ((j0 + jj) * KT + t) * 1024 + boff), ar[p][t], acc[jj]);
           const int n = j0 * 16 + nq;
           if (!STG && (!mok || n >= a.nstore)) continue;   // STG: every lane takes part in the read-back
           const int nb = min(n, NF * 16 - 8);                 // (bias reads stay inside sBias)
@@ -187,13 +190,18 @@ __global__ __launch_bounds__((64 * gs_waves<KT, NF>())) void gemm_stream_kernel(
           if constexpr (RES) {
             const u32x4 r = rr[p][j0 / 2];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) { v[2 * e] += bf_lo(r[e]); v[2 * e + 1] += bf_hi(r[e]); }
+            for (int e = 0; e < 4; ++e) { v[2 * e] += E::lo(r[e]); v[2 * e + 1] += E::hi(r[e]); }
           }
           if constexpr (ACT == 2)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-          const u32x4 o = {pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]), pack_bf16(v[4], v[5]), pack_bf16(v[6], v[7])};
+          const u32x4 o = {E::pack(v[0], v[1]), E::pack(v[2], v[3]), E::pack(v[4], v[5]), E::pack(v[6], v[7])};
           auto gstore = [&](long mm, int nn, const u32x4& val) {
+            if (a.opad == 1) {                                  // into a 1-pixel zero-bordered buffer
+              const int b = (int)(mm / OHW), rem = (int)(mm - (long)b * OHW);
+              const int oh = rem / a.OW, ow = rem - oh * a.OW;
+              mm = ((long)b * (a.OH + 2) + oh + 1) * (a.OW + 2) + ow + 1;
+            }
             if constexpr (NT) __builtin_nontemporal_store(val, (u32x4*)(a.y + mm * a.ldy + nn));
             else *(u32x4*)(a.y + mm * a.ldy + nn) = val;
           };
@@ -240,57 +248,67 @@ int num_cus() {
   return n;
 }
 
-template <int KT, int NF, bool RES, bool NT, int ACT>
+template <int KT, int NF, bool RES, bool NT, int ACT, int DT>
 hipError_t launch_act(const ConvGemmArgs& a, hipStream_t s) {
   constexpr int NW = gs_waves<KT, NF>();
   // one round of resident workgroups (by VGPRs and LDS, as the runtime computes it): a grid past
   // that runs its excess as a tail round on a fraction of the CUs
   static const int per_cu = [] {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gemm_stream_kernel<KT, NF, RES, NT, ACT>, 64 * NW, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, gemm_stream_kernel<KT, NF, RES, NT, ACT, DT>, 64 * NW, 0) != hipSuccess)
       return 1;
     return std::max(1, n);
   }();
   const long frags = (long)a.B * ((a.OH * a.OW + 15) / 16);
   const long want = (frags + NW - 1) / NW;
   const int grid = (int)std::max(1L, std::min(want, (long)num_cus() * per_cu));
-  hipLaunchKernelGGL((gemm_stream_kernel<KT, NF, RES, NT, ACT>), dim3(grid), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((gemm_stream_kernel<KT, NF, RES, NT, ACT, DT>), dim3(grid), dim3(64 * NW), 0, s, a);
   return hipGetLastError();
 }
 
-template <int KT, int NF, bool RES, bool NT>
+template <int KT, int NF, bool RES, bool NT, int DT>
 hipError_t launch_nt(const ConvGemmArgs& a, hipStream_t s) {
   switch (a.relu_out) {
-    case 0: return launch_act<KT, NF, RES, NT, 0>(a, s);
-    case 1: return launch_act<KT, NF, RES, NT, 1>(a, s);
-    case 2: return launch_act<KT, NF, RES, NT, 2>(a, s);
-    case 4: return launch_act<KT, NF, RES, NT, 4>(a, s);
+    case 0: return launch_act<KT, NF, RES, NT, 0, DT>(a, s);
+    case 1: return launch_act<KT, NF, RES, NT, 1, DT>(a, s);
+    case 2: return launch_act<KT, NF, RES, NT, 2, DT>(a, s);
+    case 4: return launch_act<KT, NF, RES, NT, 4, DT>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int KT, int NF, bool RES>
+template <int KT, int NF, bool RES, int DT>
 hipError_t launch_stream(const ConvGemmArgs& a, bool nt, hipStream_t s) {
-  return nt ? launch_nt<KT, NF, RES, true>(a, s) : launch_nt<KT, NF, RES, false>(a, s);
+  return nt ? launch_nt<KT, NF, RES, true, DT>(a, s) : launch_nt<KT, NF, RES, false, DT>(a, s);
 }
 
 // residual instances up to NF 18 (wider ones would spill the residual ring; no B7 layer has one)
-template <int KT, int NF>
+template <int KT, int NF, int DT>
 hipError_t launch_res(const ConvGemmArgs& a, bool nt, hipStream_t s) {
-  if constexpr (NF <= 18) return launch_stream<KT, NF, true>(a, nt, s);
+  if constexpr (NF <= 18) return launch_stream<KT, NF, true, DT>(a, nt, s);
   else return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-// (KT = K / 32, NF = output fragments) instances: EfficientNet-B7's large-map 1x1 convs
+// (KT = K / 32, NF = output fragments) instances: EfficientNet-B7's large-map 1x1 convs (bf16) and
+// ResNet-50's layer1 / layer2.0 1x1 convs at 56x56 (fp16: 64 -> 64, 64 -> 256, 256 -> 64, 256 -> 128)
 #define KDL_STREAM_SHAPES(X) \
   X(1, 2) X(2, 2) X(1, 12) X(6, 4) X(2, 18) X(9, 4) X(9, 6) X(3, 30) X(15, 6)
+#define KDL_STREAM_SHAPES_F16(X) \
+  X(2, 4) X(2, 16) X(8, 4) X(8, 8)
 
-bool gemm_stream_shape(int K, int nstore) {
+bool gemm_stream_shape(int K, int nstore, int dt) {
   const int kt = K / 32, nf = (nstore + 15) / 16;
-  switch (kt * 100 + nf) {
+  if (dt == 1) {
+    switch (kt * 100 + nf) {
 #define KDL_GSHAS(kt_, nf_) case kt_ * 100 + nf_:
+      KDL_STREAM_SHAPES_F16(KDL_GSHAS)
+      return K % 32 == 0;
+      default: return false;
+    }
+  }
+  switch (kt * 100 + nf) {
     KDL_STREAM_SHAPES(KDL_GSHAS)
 #undef KDL_GSHAS
     return K % 32 == 0;
@@ -299,15 +317,24 @@ bool gemm_stream_shape(int K, int nstore) {
 }
 
 hipError_t gemm_stream(const ConvGemmArgs& a, bool nt, hipStream_t s) {
-  if (a.dt != 0 || a.opad || a.stride != 1 || a.ksplit > 1 || a.OH != a.H || a.OW != a.W || a.M <= 0 ||
+  if (a.dt < 0 || a.dt > 1 || (a.dt == 1 && a.ascale) || (a.opad != 0 && a.opad != 1) || a.stride != 1 || a.ksplit > 1 || a.OH != a.H || a.OW != a.W || a.M <= 0 ||
       a.M != a.B * a.OH * a.OW || a.K % 32 != 0 || a.ldx % 8 != 0 || a.ldy % 8 != 0 || a.nstore % 8 != 0 ||
-      (a.res && a.ldr % 8 != 0) || !gemm_stream_shape(a.K, a.nstore) ||
+      (a.res && a.ldr % 8 != 0) || !gemm_stream_shape(a.K, a.nstore, a.dt) ||
       (a.ascale && (a.ascale_ld < a.K || a.ascale_ld % 4 != 0)) ||
       a.relu_out == 3 || a.relu_in || a.NF * 16 < a.nstore)
     return hipErrorInvalidValue;
+  if (a.dt == 1) {
+    switch ((a.K / 32) * 100 + (a.nstore + 15) / 16) {
+#define KDL_GSCASE1(kt_, nf_) \
+  case kt_ * 100 + nf_: return a.res ? launch_res<kt_, nf_, 1>(a, nt, s) : launch_stream<kt_, nf_, false, 1>(a, nt, s);
+      KDL_STREAM_SHAPES_F16(KDL_GSCASE1)
+#undef KDL_GSCASE1
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch ((a.K / 32) * 100 + (a.nstore + 15) / 16) {
 #define KDL_GSCASE(kt_, nf_) \
-  case kt_ * 100 + nf_: return a.res ? launch_res<kt_, nf_>(a, nt, s) : launch_stream<kt_, nf_, false>(a, nt, s);
+  case kt_ * 100 + nf_: return a.res ? launch_res<kt_, nf_, 0>(a, nt, s) : launch_stream<kt_, nf_, false, 0>(a, nt, s);
     KDL_STREAM_SHAPES(KDL_GSCASE)
 #undef KDL_GSCASE
     default: return hipErrorInvalidValue;

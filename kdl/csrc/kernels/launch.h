@@ -106,7 +106,7 @@ int sepconv_2d_config(int cfg, int* bm, int* bn, int* threads);
 // only; per-image weights ok).
 constexpr int STREAM_CFG_BASE = 3000;
 hipError_t gemm_stream(const ConvGemmArgs& a, bool nt, hipStream_t s);
-bool gemm_stream_shape(int K, int nstore);
+bool gemm_stream_shape(int K, int nstore, int dt = 0);
 hipError_t conv_gemm(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 hipError_t gemm_pipe(int mode, int cfg, const ConvGemmArgs& a, hipStream_t s);
 int gemm_pipe_config(int cfg, int* bm, int* bn, int* threads);

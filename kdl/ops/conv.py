@@ -90,13 +90,15 @@ SEPW_XB = {120: 9, 121: 9, 122: 11, 123: 16, 124: 9, 125: 8, 126: 9, 127: 9,
 # (gemm_pipe.hip ConvGemmArgs.ksplit): SPLITK_BASE + 100 * ksplit + base id
 SPLITK_BASE = 2000
 # STREAM_BASE: persistent streaming pointwise GEMM with the weights resident in LDS (gemm_stream.hip;
-# MODE_PW stride 1, bf16; only the (K/32, ldy/16) instances in STREAM_SHAPES -- EfficientNet-B7's
-# large-map expand / project convs). Stores all ldy channels, so its nominal tile is 16 x 32.
+# MODE_PW stride 1; only the (K/32, ldy/16) instances in STREAM_SHAPES (bf16: EfficientNet-B7's
+# large-map expand / project convs) and STREAM_SHAPES_F16 (fp16: ResNet-50's 56x56 1x1 convs)). Stores all ldy channels, so its nominal tile is 16 x 32.
 # STREAM_NT: the same with nontemporal output stores (outputs far past the 256 MB MALL).
 STREAM_BASE = 3000
 STREAM_NT = 3001
 STREAM_IDS = (STREAM_BASE, STREAM_NT)
 STREAM_SHAPES = frozenset([(1, 2), (2, 2), (1, 12), (6, 4), (2, 18), (9, 4), (9, 6), (3, 30), (15, 6)])
+# fp16 instances (dt 1): ResNet-50's layer1 / layer2.0 1x1 convs at 56x56 (gemm_stream.hip KDL_STREAM_SHAPES_F16)
+STREAM_SHAPES_F16 = frozenset([(2, 4), (2, 16), (8, 4), (8, 8)])
 # never autotune candidates: the ws stamping build and band ablation
 ABLATION_IDS = frozenset([127, 147, 128, 129, 130, 131, 132, 133])
 
@@ -261,8 +263,9 @@ class ConvGemmLayer:
         the packed weights must hold all ldy / 16 fragments; residual instances up to ldy 288)."""
         if res and self.ldy > 288:
             return False
-        return (self.mode == MODE_PW and self.stride == 1 and self.dt == 0 and not self.relu_in
-                and self.relu_out != 3 and (self.K // 32, self.ldy // 16) in STREAM_SHAPES
+        shapes = STREAM_SHAPES if self.dt == 0 else STREAM_SHAPES_F16
+        return (self.mode == MODE_PW and self.stride == 1 and not self.relu_in
+                and self.relu_out != 3 and (self.K // 32, self.ldy // 16) in shapes
                 and self.nf_max * 16 >= self.ldy)
 
     def dw_args(self, x: int, tmp: int, g: Geometry, ldx: int | None = None) -> dict:

@@ -91,6 +91,45 @@ def test_relu_after_residual(dt):
     assert (y.float() >= 0).all()
 
 
+@pytest.mark.parametrize("K,N,kind", [(64, 64, "relu"), (64, 256, "res_relu"), (64, 256, "plain"),
+                                      (256, 64, "relu"), (256, 128, "relu"), (64, 64, "relu_opad"),
+                                      (256, 128, "relu_opad")])
+@pytest.mark.parametrize("cfg_name", ["STREAM_BASE", "STREAM_NT"])
+def test_gemm_stream_fp16(K, N, kind, cfg_name):
+    """Streaming pointwise GEMM in fp16 (gemm_stream.hip DT 1): ResNet-50's 56x56 1x1 convs
+    (conv1 64/256 -> 64, layer2.0.conv1 256 -> 128, conv3 / downsample 64 -> 256 with and without
+    the residual + ReLU) on a ragged 29x29 map, against fp32."""
+    from kdl.ops import conv as CV
+    cfg = getattr(CV, cfg_name)
+    gen = torch.Generator().manual_seed(K + N)
+    dt = torch.float16
+    B, H = 3, 29
+    x = torch.randn(B * H * H, K, generator=gen).to(dt)
+    r = torch.randn(B * H * H, N, generator=gen).to(dt)
+    w = torch.randn(N, K, generator=gen, dtype=torch.float64) / K ** 0.5
+    b = torch.randn(N, generator=gen) * 0.1
+    relu_out = {"relu": 1, "res_relu": 2, "plain": 0, "relu_opad": 1}[kind]
+    opad = int(kind == "relu_opad")
+    lay = ConvGemmLayer("s", MODE_PW, w, b, cin_pad=K, n=N, relu_out=relu_out, device=DEV, dtype=dt)
+    assert lay.stream_ok(res=kind == "res_relu") and (False, cfg) in lay.variants(H)
+    P = H + 2 * opad
+    y = torch.zeros(B * P * P * lay.ldy, dtype=dt, device=DEV)
+    res = r.to(DEV).contiguous() if kind == "res_relu" else None
+    lay.launch(x.to(DEV).contiguous(), y, Geometry(B, H, H, H, H), res=res, cfg=cfg, opad=opad)
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().t() + b
+    if kind == "res_relu":
+        ref = torch.relu(ref + r.float())
+    elif kind != "plain":
+        ref = torch.relu(ref)
+    yv = y.cpu().view(B, P, P, lay.ldy)
+    if opad:                                   # interior = the result, the 1-pixel border stays zero
+        assert yv[:, 0].abs().max() == 0 and yv[:, -1].abs().max() == 0
+        assert yv[:, :, 0].abs().max() == 0 and yv[:, :, -1].abs().max() == 0
+        yv = yv[:, 1:-1, 1:-1]
+    assert _rel(yv.reshape(-1, lay.ldy)[:, :N], ref) < 4e-3
+
+
 def test_gap_fc():
     gen = torch.Generator().manual_seed(4)
     B, HW, Fd, N = 11, 49, 2048, 1000
