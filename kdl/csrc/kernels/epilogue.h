@@ -60,4 +60,22 @@ __device__ __forceinline__ void epi_store(const ConvGemmArgs& a, int m, int n, u
   *(u32x4*)(a.y + out_offset(a, m) + n) = v;
 }
 
+// epi_store with the residual already loaded (rv; ignored when a.res is null): the caller issued
+// the residual loads ahead of the store pass, so no load waits behind the pass's stores in the
+// in-order vmcnt
+template <int DT = 0>
+__device__ __forceinline__ void epi_store_r(const ConvGemmArgs& a, int m, int n, u32x4 v, const u32x4 rv) {
+  using E = Elt<DT>;
+  if (a.relu_out >= 3) v = act_transcendental<DT>(a.relu_out, v);
+  if (a.res) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[d] = E::pack(E::lo(v[d]) + E::lo(rv[d]), E::hi(v[d]) + E::hi(rv[d]));
+  }
+  if (a.relu_out == 2) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) v[d] = relu_bf16x2(v[d]);
+  }
+  *(u32x4*)(a.y + out_offset(a, m) + n) = v;
+}
+
 }  // namespace kdl
