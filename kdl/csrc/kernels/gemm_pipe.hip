@@ -249,12 +249,28 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_pipe_kernel(ConvGemmArgs 
       *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){E::pack(v0, v1), E::pack(v2, v3)};
     }
   }
-  __syncthreads();
+  // residual rows (ResNet conv3, ViT out_proj / mlp.3): loaded now, with the accumulators already in
+  // LDS, instead of inside the store pass where each load waited behind the earlier stores
+  // (in-order vmcnt; the same change in sepconv_ws.hip: profiles/middle_flow_r6.txt section 7).
+  // Interleaved bench pairs: ResNet-50 +1.6 %, ViT-B/16 bf16 +0.7 % (profiles/epilogue_residual_r6.txt)
   constexpr int CPR = BN / 8;
-  for (int c = tid; c < BM * CPR; c += 64 * NW) {
-    const int r = c / CPR, cc = c - r * CPR;
+  constexpr int NIT = (BM * CPR + 64 * NW - 1) / (64 * NW);
+  u32x4 rres[NIT];
+  if (a.res) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = tid + it * 64 * NW, r = c / CPR, cc = c - r * CPR;
+      const int m = min(m0 + r, a.M - 1), n = min(n0 + cc * 8, a.nstore - 8);
+      rres[it] = c < BM * CPR ? *(const u32x4*)(a.res + (long)m * a.ldr + n) : (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = tid + it * 64 * NW, r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
-    if (m < mend && n < a.nstore) epi_store<DT>(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16));
+    if (c < BM * CPR && m < mend && n < a.nstore)
+      epi_store_r<DT>(a, m, n, *(const u32x4*)(smem + r * CS + cc * 16), rres[it]);
   }
 }
 
