@@ -136,16 +136,30 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_f8_kernel(GemmF8Args a) {
       *(u32x2*)(smem + ml * CS + nl * 2) = (u32x2){pack_bf16(v0, v1), pack_bf16(v2, v3)};
     }
   }
-  __syncthreads();
+  // residual rows (ViT out_proj / mlp.3): loaded before the C-tile barrier, not inside the store pass
+  // where each load waited behind the earlier stores (in-order vmcnt; cf. gemm_pipe.hip / sepconv_ws.hip):
+  // ViT-B/16 fp8 +1.2 % in 3 of 3 interleaved pairs (profiles/epilogue_residual_r6.txt)
   constexpr int CPR = BN / 8;
-  for (int c = tid; c < BM * CPR; c += 64 * NW) {
-    const int r = c / CPR, cc = c - r * CPR;
+  constexpr int NIT = (BM * CPR + 64 * NW - 1) / (64 * NW);
+  u32x4 rres[NIT];
+  if (a.res) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int c = tid + it * 64 * NW, r = c / CPR, cc = c - r * CPR;
+      const int m = min(m0 + r, a.M - 1), n = min(n0 + cc * 8, a.nstore - 8);
+      rres[it] = c < BM * CPR ? *(const u32x4*)(a.res + (long)m * a.ldr + n) : (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int c = tid + it * 64 * NW, r = c / CPR, cc = c - r * CPR;
     const int m = m0 + r, n = n0 + cc * 8;
-    if (m < a.M && n < a.nstore) {
+    if (c < BM * CPR && m < a.M && n < a.nstore) {
       u32x4 v = *(const u32x4*)(smem + r * CS + cc * 16);
       if (a.relu_out >= 3) v = act_transcendental(a.relu_out, v);
       if (a.res) {
-        const u32x4 rv = *(const u32x4*)(a.res + (long)m * a.ldr + n);
+        const u32x4 rv = rres[it];
 #pragma unroll
         for (int d = 0; d < 4; ++d) v[d] = pack_bf16(bf_lo(v[d]) + bf_lo(rv[d]), bf_hi(v[d]) + bf_hi(rv[d]));
       }
